@@ -1,0 +1,222 @@
+/*
+ * mm_oracle.c -- CPU restatement of the reference flow step (TEST INFRASTRUCTURE).
+ * Contract and citations: mm_oracle.h. Build: make -C oracle oracle
+ * (-ffp-contract=off, no fast-math: every operation is one IEEE-754 binary64
+ * operation in the order written, the same order the HIP kernels use).
+ */
+#include "mm_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+long long or_step_count(double time, double time_step) {
+    /* Model.hpp:48. Guard: a non-positive step never terminates in the reference. */
+    if (!(time_step > 0.0)) return -1;
+    long long n = 0;
+    for (double t = 0; t < time; t = t + time_step) ++n;
+    return n;
+}
+
+void or_partition_reference(int H, int W, int P, int k,
+                            int* x_init, int* y_init, int* height, int* width) {
+    /* Model.hpp:63-64,70-75: count = (H*W)/P; worker k gets offset (k-1)*count. */
+    int count = (H * W) / P;
+    int offset = (k - 1) * count;
+    *x_init = offset / W;
+    *y_init = 0; /* cellular_space.y_init of the caller's space, 0 in Main.cpp:25 */
+    *height = H / P;
+    *width = W;
+}
+
+int or_owner_reference(int H, int P, int x) {
+    return (x / (H / P)) + 1; /* Model.hpp:80 */
+}
+
+void or_partition_rows(long long H, int G, int g, long long* x_init, long long* h) {
+    long long a = (g * H) / G;
+    long long b = ((g + 1) * H) / G;
+    *x_init = a;
+    *h = b - a;
+}
+
+static inline long long span3(long long n, long long i) {
+    long long c = 1;
+    if (i > 0) ++c;
+    if (i < n - 1) ++c;
+    return c;
+}
+
+int or_neighbor_count(long long H, long long W, long long x, long long y) {
+    if (x < 0 || y < 0 || x >= H || y >= W) return 0;
+    return (int)(span3(H, x) * span3(W, y) - 1);
+}
+
+static inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+void or_fill_random(long long H, long long W, long long x_init, long long h,
+                    uint64_t seed, double* out) {
+    (void)H;
+    for (long long i = 0; i < h; ++i)
+        for (long long y = 0; y < W; ++y) {
+            uint64_t gidx = (uint64_t)((x_init + i) * W + y);
+            uint64_t z = splitmix64(seed ^ gidx);
+            double u = (double)(z >> 11) * 0x1.0p-53;
+            out[i * W + y] = 1.0 + u;
+        }
+}
+
+/* share of one emitter: s = out / cnt, cnt == 8 as the exact *0.125 */
+static inline double share_of(double out, int cnt) {
+    if (cnt == 8) return out * 0.125;
+    if (cnt <= 0) return 0.0;
+    return out / (double)cnt;
+}
+
+void or_point_apply(long long H, long long W, double* v, long long sx, long long sy,
+                    double captured, double rate) {
+    int cnt = or_neighbor_count(H, W, sx, sy);
+    if (cnt <= 0) return;
+    double out = rate * captured;          /* Exponencial.hpp:15 */
+    double share = share_of(out, cnt);     /* Model.hpp:199 */
+    for (long long dx = -1; dx <= 1; ++dx)
+        for (long long dy = -1; dy <= 1; ++dy) {
+            long long x = sx + dx, y = sy + dy;
+            if ((dx == 0 && dy == 0) || x < 0 || y < 0 || x >= H || y >= W) continue;
+            v[x * W + y] = v[x * W + y] + share;    /* Model.hpp:206-209,234 */
+        }
+    v[sx * W + sy] = v[sx * W + sy] - out;          /* Model.hpp:211 */
+}
+
+/* s row of global row gx (NULL vrow or outside grid -> +0.0) */
+static void s_row(long long H, long long W, long long gx, const double* vrow,
+                  double rate, double* s) {
+    if (vrow == NULL || gx < 0 || gx >= H) {
+        for (long long y = 0; y < W; ++y) s[y] = 0.0;
+        return;
+    }
+    for (long long y = 0; y < W; ++y) {
+        int cnt = or_neighbor_count(H, W, gx, y);
+        double out = cnt > 0 ? rate * vrow[y] : 0.0;
+        s[y] = share_of(out, cnt);
+    }
+}
+
+/* rows(gx) gives the v row for any global gx in [x_lo-1, x_hi]. */
+typedef const double* (*row_fn)(const void* ctx, long long gx);
+
+static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
+                      row_fn rows, const void* ctx, double* vout, double rate) {
+    double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
+    double* s_prev = buf;
+    double* s_cur = buf + W;
+    double* s_next = buf + 2 * W;
+    double* p = buf + 3 * W;
+    double* c3 = buf + 4 * W; /* W+2 entries, c3[y+1] for column y */
+    c3[0] = 0.0;
+    c3[W + 1] = 0.0;
+    s_row(H, W, x_lo - 1, rows(ctx, x_lo - 1), rate, s_prev);
+    s_row(H, W, x_lo, rows(ctx, x_lo), rate, s_cur);
+    for (long long x = x_lo; x < x_hi; ++x) {
+        s_row(H, W, x + 1, rows(ctx, x + 1), rate, s_next);
+        for (long long y = 0; y < W; ++y) {
+            p[y] = s_prev[y] + s_next[y];
+            c3[y + 1] = p[y] + s_cur[y];
+        }
+        const double* v = rows(ctx, x);
+        double* o = vout + (x - x_lo) * W;
+        for (long long y = 0; y < W; ++y) {
+            int cnt = or_neighbor_count(H, W, x, y);
+            double out = cnt > 0 ? rate * v[y] : 0.0;
+            double nb = (c3[y] + c3[y + 2]) + p[y];
+            o[y] = (v[y] - out) + nb;
+        }
+        double* t = s_prev;
+        s_prev = s_cur;
+        s_cur = s_next;
+        s_next = t;
+    }
+    free(buf);
+}
+
+typedef struct {
+    const double* v;
+    long long H, W, base; /* v row 0 is global row `base` */
+    long long lo, hi;     /* valid global rows [lo, hi) */
+} grid_ctx;
+
+static const double* grid_row(const void* ctx_, long long gx) {
+    const grid_ctx* c = (const grid_ctx*)ctx_;
+    if (gx < c->lo || gx >= c->hi || gx < 0 || gx >= c->H) return NULL;
+    return c->v + (gx - c->base) * c->W;
+}
+
+void or_field_step(long long H, long long W, const double* v, double* vout, double rate) {
+    grid_ctx c = {v, H, W, 0, 0, H};
+    step_rows(H, W, 0, H, grid_row, &c, vout, rate);
+}
+
+void or_field_step_slab(long long H, long long W, long long x_init, long long h,
+                        const double* vg, double* vout, double rate) {
+    grid_ctx c = {vg, H, W, x_init - 1, x_init - 1, x_init + h + 1};
+    step_rows(H, W, x_init, x_init + h, grid_row, &c, vout, rate);
+}
+
+void or_field_step_general(long long H, long long W, const double* v, const double* outf,
+                           double* vout) {
+    double* s = (double*)malloc(sizeof(double) * (size_t)(H * W));
+    for (long long x = 0; x < H; ++x)
+        for (long long y = 0; y < W; ++y)
+            s[x * W + y] = share_of(outf[x * W + y], or_neighbor_count(H, W, x, y));
+#define S(x, y) (((x) < 0 || (y) < 0 || (x) >= H || (y) >= W) ? 0.0 : s[(x) * W + (y)])
+    for (long long x = 0; x < H; ++x)
+        for (long long y = 0; y < W; ++y) {
+            double p = S(x - 1, y) + S(x + 1, y);
+            double c3l = (S(x - 1, y - 1) + S(x + 1, y - 1)) + S(x, y - 1);
+            double c3r = (S(x - 1, y + 1) + S(x + 1, y + 1)) + S(x, y + 1);
+            double nb = (c3l + c3r) + p;
+            vout[x * W + y] = (v[x * W + y] - outf[x * W + y]) + nb;
+        }
+#undef S
+    free(s);
+}
+
+void or_program_step(long long H, long long W, int n_attr, double* const* v,
+                     const or_flow* flows, int n_flows, double* scratch) {
+    const long long n = H * W;
+    for (int f = 0; f < n_flows; ++f) {
+        const or_flow* fl = &flows[f];
+        if (fl->a < 0 || fl->a >= n_attr) continue;
+        if (fl->kind == 1) {
+            or_field_step(H, W, v[fl->a], scratch, fl->rate);
+            memcpy(v[fl->a], scratch, sizeof(double) * (size_t)n);
+        } else if (fl->kind == 2) {
+            double* va = v[fl->a];
+            double* vb = (fl->b >= 0 && fl->b < n_attr) ? v[fl->b] : NULL;
+            for (long long i = 0; i < n; ++i) {
+                double out = fl->rate * va[i];
+                va[i] = va[i] - out;
+                if (vb) vb[i] = vb[i] + out;
+            }
+        }
+    }
+}
+
+double or_sum(const double* v, size_t n) {
+    double s = 0.0, c = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        double x = v[i];
+        double t = s + x;
+        if (fabs(s) >= fabs(x))
+            c += (s - t) + x;
+        else
+            c += (x - t) + s;
+        s = t;
+    }
+    return s + c;
+}

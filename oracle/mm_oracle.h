@@ -1,0 +1,102 @@
+/*
+ * mm_oracle -- CPU restatement of daviidsilvaa/MPI-Model's flow step.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the checker the HIP path is compared with;
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it. The product (libmpimodel_hip.so, mpi-model_amd/) never links or calls it.
+ *
+ * Pinning: the single-source application (or_point_apply) is checked bit-exactly
+ * against golden grids produced by the reference itself (tests/golden/, made by
+ * tests/golden/make_golden.py from oracle/_ref/). The generalised whole-grid,
+ * multi-step step (or_field_step*) has no reference implementation (the
+ * reference's time loop is commented out, Model.hpp:180-183); it is pinned
+ * through the single-source case (rate zero everywhere but the source reduces
+ * it to Model.hpp:176-235 bit-for-bit) plus invariants (conservation, flip
+ * symmetry, uniform fixed point). See DESIGN.md section "Oracle".
+ *
+ * Arithmetic contract (shared with the HIP kernels, compiled -ffp-contract=off):
+ *   out(c) = r * v(c)                                   Exponencial.hpp:18-20
+ *   s(c)   = out(c) / cnt(c)   (cnt==8: out*0.125, exact) Model.hpp:199
+ *   p(c)   = s(x-1,y) + s(x+1,y)
+ *   c3(c)  = p(c) + s(c)
+ *   nb(c)  = (c3(x,y-1) + c3(x,y+1)) + p(c)
+ *   v'(c)  = (v(c) - out(c)) + nb(c)                    Model.hpp:206-211,234
+ * s is +0.0 outside the global grid; cnt is the number of in-grid Moore
+ * neighbours (Cell.hpp:71-157 gives 3/5/8 for grids of at least 2x2).
+ */
+#ifndef MM_ORACLE_H
+#define MM_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Model.hpp:47-51: for(double t = 0; t < time; t = t + time_step) -- count only. */
+long long or_step_count(double time, double time_step);
+
+/* Model.hpp:60-76: worker k (1-based) of P = comm_size-1 workers. int arithmetic,
+ * exactly as the reference (remainder rows silently dropped). */
+void or_partition_reference(int H, int W, int P, int k,
+                            int* x_init, int* y_init, int* height, int* width);
+/* Model.hpp:80: owner rank of row x. */
+int or_owner_reference(int H, int P, int x);
+
+/* Balanced row partition used by the engine: part g of G gets rows
+ * [floor(g*H/G), floor((g+1)*H/G)). Equal to or_partition_reference when G | H. */
+void or_partition_rows(long long H, int G, int g, long long* x_init, long long* h);
+
+/* Cell.hpp:71-157 generalised: number of in-grid Moore neighbours of (x,y). */
+int or_neighbor_count(long long H, long long W, long long x, long long y);
+
+/* Deterministic synthetic input keyed by GLOBAL cell index:
+ * v = 1 + u, u = (splitmix64(seed ^ (x*W+y)) >> 11) * 2^-53. Rows
+ * [x_init, x_init+h) into out[h*W]. */
+void or_fill_random(long long H, long long W, long long x_init, long long h,
+                    uint64_t seed, double* out);
+
+/* Model.hpp:176-235: the single-source application on a full H x W grid, the
+ * source's outflow from the Flow's captured value (Exponencial.hpp:14-16). */
+void or_point_apply(long long H, long long W, double* v, long long sx, long long sy,
+                    double captured, double rate);
+
+/* One generalised step on the full grid (Jacobi, v -> vout). */
+void or_field_step(long long H, long long W, const double* v, double* vout, double rate);
+
+/* One generalised step on a row slab with ghost rows: vg has (h+2) rows of W,
+ * row 0 = global row x_init-1, row h+1 = global row x_init+h (ignored when
+ * outside the grid). Writes h rows to vout. */
+void or_field_step_slab(long long H, long long W, long long x_init, long long h,
+                        const double* vg, double* vout, double rate);
+
+/* The same step with an arbitrary per-cell outflow field outf (instead of
+ * r*v): s = outf/cnt, v' = (v - outf) + nb. With outf = r*v it is
+ * or_field_step bit-for-bit; with outf zero except r*captured at the source it
+ * is or_point_apply bit-for-bit -- the algebraic link between the generalised
+ * step and the reference's single-source update (Model.hpp:176-235). */
+void or_field_step_general(long long H, long long W, const double* v, const double* outf,
+                           double* vout);
+
+/* Multi-attribute flow program (config C5). Each flow is applied in declared
+ * order to the whole grid; a step applies all of them once.
+ *   kind 1 = DIFFUSE  : Exponencial of attribute a to its Moore neighbours
+ *   kind 2 = TRANSFER : out = r*v_a; v_a -= out; v_b += out (b < 0: sink)  */
+typedef struct {
+    int kind;
+    int a;
+    int b;
+    double rate;
+} or_flow;
+
+void or_program_step(long long H, long long W, int n_attr, double* const* v,
+                     const or_flow* flows, int n_flows, double* scratch);
+
+/* Neumaier-compensated sum (used for quick checks; tests use math.fsum). */
+double or_sum(const double* v, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

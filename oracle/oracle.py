@@ -1,0 +1,148 @@
+"""ctypes front-end of the C oracle (oracle/mm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker. The product path never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libmm_oracle.so")
+
+SEED = 0x4D50494D
+
+_lib = None
+
+
+class OrFlow(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("a", ctypes.c_int), ("b", ctypes.c_int),
+                ("rate", ctypes.c_double)]
+
+
+DIFFUSE = 1
+TRANSFER = 2
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        LL, D, I, P = ctypes.c_longlong, ctypes.c_double, ctypes.c_int, ctypes.c_void_p
+        L.or_step_count.restype = LL
+        L.or_step_count.argtypes = [D, D]
+        L.or_partition_reference.argtypes = [I, I, I, I] + [ctypes.POINTER(I)] * 4
+        L.or_owner_reference.restype = I
+        L.or_owner_reference.argtypes = [I, I, I]
+        L.or_partition_rows.argtypes = [LL, I, I, ctypes.POINTER(LL), ctypes.POINTER(LL)]
+        L.or_neighbor_count.restype = I
+        L.or_neighbor_count.argtypes = [LL, LL, LL, LL]
+        L.or_fill_random.argtypes = [LL, LL, LL, LL, ctypes.c_uint64, P]
+        L.or_point_apply.argtypes = [LL, LL, P, LL, LL, D, D]
+        L.or_field_step.argtypes = [LL, LL, P, P, D]
+        L.or_field_step_slab.argtypes = [LL, LL, LL, LL, P, P, D]
+        L.or_field_step_general.argtypes = [LL, LL, P, P, P]
+        L.or_program_step.argtypes = [LL, LL, I, P, ctypes.POINTER(OrFlow), I, P]
+        L.or_sum.restype = D
+        L.or_sum.argtypes = [P, ctypes.c_size_t]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def step_count(time, dt):
+    return lib().or_step_count(time, dt)
+
+
+def partition_reference(H, W, P, k):
+    o = [ctypes.c_int() for _ in range(4)]
+    lib().or_partition_reference(H, W, P, k, *[ctypes.byref(x) for x in o])
+    return tuple(x.value for x in o)  # x_init, y_init, height, width
+
+
+def owner_reference(H, P, x):
+    return lib().or_owner_reference(H, P, x)
+
+
+def partition_rows(H, G, g):
+    a, h = ctypes.c_longlong(), ctypes.c_longlong()
+    lib().or_partition_rows(H, G, g, ctypes.byref(a), ctypes.byref(h))
+    return a.value, h.value
+
+
+def neighbor_count(H, W, x, y):
+    return lib().or_neighbor_count(H, W, x, y)
+
+
+def fill_random(H, W, x_init=0, h=None, seed=SEED):
+    h = H if h is None else h
+    out = np.empty((h, W), dtype=np.float64)
+    lib().or_fill_random(H, W, x_init, h, seed, _ptr(out))
+    return out
+
+
+def point_apply(v, sx, sy, captured, rate):
+    v = np.ascontiguousarray(v, dtype=np.float64).copy()
+    H, W = v.shape
+    lib().or_point_apply(H, W, _ptr(v), sx, sy, captured, rate)
+    return v
+
+
+def field_step(v, rate, steps=1):
+    v = np.ascontiguousarray(v, dtype=np.float64).copy()
+    H, W = v.shape
+    o = np.empty_like(v)
+    for _ in range(steps):
+        lib().or_field_step(H, W, _ptr(v), _ptr(o), rate)
+        v, o = o, v
+    return v
+
+
+def field_step_general(v, outf):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    outf = np.ascontiguousarray(outf, dtype=np.float64)
+    H, W = v.shape
+    o = np.empty_like(v)
+    lib().or_field_step_general(H, W, _ptr(v), _ptr(outf), _ptr(o))
+    return o
+
+
+def field_step_slab(H, W, x_init, vg, rate):
+    """vg: (h+2, W) slab with ghost rows; returns (h, W)."""
+    vg = np.ascontiguousarray(vg, dtype=np.float64)
+    h = vg.shape[0] - 2
+    o = np.empty((h, W), dtype=np.float64)
+    lib().or_field_step_slab(H, W, x_init, h, _ptr(vg), _ptr(o), rate)
+    return o
+
+
+def program_step(fields, flows, steps=1, sums_per_step=False):
+    """fields: list of (H, W) arrays (one per attribute); flows: [(kind, a, b, rate)]."""
+    fields = [np.ascontiguousarray(f, dtype=np.float64).copy() for f in fields]
+    H, W = fields[0].shape
+    arr = (ctypes.c_void_p * len(fields))(*[f.ctypes.data for f in fields])
+    fl = (OrFlow * len(flows))(*[OrFlow(k, a, b, r) for k, a, b, r in flows])
+    scratch = np.empty((H, W), dtype=np.float64)
+    sums = []
+    for _ in range(steps):
+        lib().or_program_step(H, W, len(fields), arr, fl, len(flows), _ptr(scratch))
+        if sums_per_step:
+            sums.append([float(np.sum(f, dtype=np.float64)) for f in fields])
+    return (fields, sums) if sums_per_step else fields
+
+
+def csum(v):
+    v = np.ascontiguousarray(v, dtype=np.float64).ravel()
+    return lib().or_sum(_ptr(v), v.size)
