@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X engine on the reference's headline metric.
+
+metric  : cell-updates/s (GCUPS) of the generalised Exponencial flow step
+          (BASELINE.json), whole job over all ranks, + % of the HBM roofline
+workload: default "c2" = BASELINE.json configs[1]: 4096 x 4096 fp64 cells per GPU,
+          one Exponencial flow (rate 0.1, src/Main.cpp:33), 1000 steps. With
+          --gpus N the grid is (4096*N) x 4096, one row slab per GPU, border rows
+          exchanged over RCCL every step (weak scaling). Other workloads:
+          c3 (32768^2 strong), c4 (16384^2 per GPU, weak), c5 (4 attributes,
+          chained transfers + 4 diffusions, per-step sums).
+step    : one pass of the flow over the whole grid (all passes of the program).
+timing  : W untimed warmup steps, then exactly K steps bracketed by a barrier and
+          torch.cuda.synchronize() on both sides; the max over ranks is reported.
+          Inputs are resident in HBM (generated on the device) before timing.
+
+Launch: python bench.py [--gpus 1] [--steps 1000] [--warmup 50]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mpi-model_amd"))
+
+import mpimodel as mm  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+RATE = 0.1             # src/Main.cpp:33
+
+WORKLOADS = {
+    # name: (rows per GPU or global rows, cols, scaling, n_attr)
+    "c2": dict(rows=4096, cols=4096, scaling="weak", n_attr=1,
+               desc="4096x4096 fp64 per GPU, one Exponencial flow (BASELINE configs[1])"),
+    "c3": dict(rows=32768, cols=32768, scaling="strong", n_attr=1,
+               desc="32768x32768 fp64 global, row slabs (BASELINE configs[2])"),
+    "c4": dict(rows=16384, cols=16384, scaling="weak", n_attr=1,
+               desc="16384x16384 fp64 per GPU (BASELINE configs[3])"),
+    "c5": dict(rows=4096, cols=4096, scaling="weak", n_attr=4,
+               desc="4 attributes, 4 chained transfers + 4 diffusions, per-step sums "
+                    "(BASELINE configs[4])"),
+}
+
+C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
+            (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-baseline sample length (oracle port, rank 0, N=1)")
+    return ap.parse_args()
+
+
+def cpu_baseline(H, W, seconds):
+    """The oracle's scalar C port of the same step (oracle/mm_oracle.c), one core, on a
+    bounded sample: as many whole steps of the same grid as fit in `seconds`."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle
+    v = oracle.fill_random(H, W)
+    o = np.empty_like(v)
+    L = oracle.lib()
+    ptr = oracle._ptr
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        L.or_field_step(H, W, ptr(v), ptr(o), RATE)
+        v, o = o, v
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 10000:
+            break
+    return {"value": H * W * steps / el / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
+            "sample": f"{steps} steps of the {H}x{W} fp64 grid, oracle/mm_oracle.c "
+                      f"or_field_step (scalar C, -O2), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    wl = WORKLOADS[args.workload]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus N > 1 needs one process per GPU (torch.distributed.run)")
+    N = world
+
+    import torch
+    import torch.distributed as dist
+    if N > 1:
+        dist.init_process_group("gloo")  # control plane only; data moves on RCCL
+
+    if wl["scaling"] == "weak":
+        H = wl["rows"] * N
+    else:
+        H = wl["rows"]
+    W = wl["cols"]
+    x0, h = mm.partition_rows(H, N, rank)
+
+    if N > 1:
+        ids = [mm.comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        eng = mm.Engine(H, W, x0, h, n_attr=wl["n_attr"], device=local, rank=rank, nranks=N,
+                        halo_mode=mm.MM_HALO_RCCL, comm_id_bytes=ids[0])
+    else:
+        eng = mm.Engine(H, W, n_attr=wl["n_attr"], device=local)
+    torch.cuda.set_device(local)
+
+    na = wl["n_attr"]
+    for a in range(na):
+        eng.fill_random(a, seed=mm.SEED + a)
+    if args.workload == "c5":
+        for kind, a, b, r in C5_FLOWS:
+            if kind == 1:
+                eng.add_diffuse(a, r)
+            else:
+                eng.add_transfer(a, b, r)
+        reduce_every = 1
+    else:
+        eng.add_diffuse(0, RATE)
+        reduce_every = 0
+    s_before = eng.sums()
+
+    # warmup (graph capture, clocks, caches)
+    eng.run(args.warmup, reduce_every)
+    eng.synchronize()
+
+    # timed region: at N=1 every step kernel is bracketed by HIP events on its stream
+    eng.set_timing(True)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run(args.steps, reduce_every)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if N > 1:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n_launch, kern_ms, bytes_per_launch = eng.timing()
+    s_after = eng.sums()
+    info = eng.info()
+
+    cells = H * W
+    gcups = cells * args.steps / el / 1e9
+    if rank == 0:
+        kern_avg_ms = kern_ms / max(n_launch, 1)
+        launches_per_step = n_launch / max(args.steps, 1)
+        achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
+        traffic = None
+        tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get(f"{args.workload}_n{N}_bytes_per_launch")
+        cons = [abs(float(b) - float(a)) / abs(float(a)) for a, b in zip(s_before, s_after)]
+        line = {
+            "metric": "cell-updates/s (GCUPS) per step + % of HBM roofline",
+            "value": round(gcups, 3),
+            "unit": "GCUPS",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": wl["scaling"],
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
+                    "seed 0x4D50494D, generated on the device",
+            "config": {"workload": f"{args.workload}: {wl['desc']}", "grid": [H, W],
+                       "rows_per_gpu": h, "n_attr": na, "rate": RATE,
+                       "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else ""),
+                       "passes_per_step": info["n_passes"],
+                       "rows_per_wave": info["rows_per_wave"]},
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic,
+                "kernel": "mm_pass_kernel",
+                "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "launches_per_step": launches_per_step,
+            },
+            "check": {"sum_rel_drift": max(cons)},
+        }
+        if N == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
+                if na == 1 else None
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if N > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * mpimodel.h -- C ABI of the MI355X engine for MPI-Model's flow step.
+ *
+ * This is the drop-in boundary: plain C types, plain pointers and sizes, no
+ * torch or HIP types. It is called by
+ *   - the C++ API headers (mpi-model_amd/api/Model.hpp & co.), which keep the
+ *     reference's Model / CellularSpace / Cell / Attribute / Flow / Exponencial
+ *     classes so a Main.cpp-style program builds unchanged, and
+ *   - Python through ctypes (mpi-model_amd/mpimodel.py), used by bench.py/tests.
+ * Implementation: mpi-model_amd/csrc/ -> libmpimodel_hip.so (gfx950 only).
+ *
+ * Each entry point names the reference code it replaces (paths relative to the
+ * reference repository root). The reference has no C ABI of its own; its
+ * boundary is the C++ template API. INTEGRATION.md shows how a
+ * reference Model::execute binds to these calls.
+ *
+ * Errors: every int-returning call returns MM_OK (0) or an MM_ERR_* code and
+ * stores a message retrievable with mm_last_error() (thread-local). The C++
+ * layer turns non-zero codes into std::runtime_error, as src/MPIImpl.cpp:7-8,13-14
+ * does for MPI failures.
+ */
+#ifndef MPIMODEL_H
+#define MPIMODEL_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_ABI_VERSION 1
+
+enum mm_status {
+    MM_OK = 0,
+    MM_ERR_INVALID = 1,     /* bad argument / shape */
+    MM_ERR_HIP = 2,         /* HIP runtime failure (no device, launch failure, ...) */
+    MM_ERR_RCCL = 3,        /* RCCL failure in the halo exchange */
+    MM_ERR_STATE = 4,       /* call not valid in the engine's current state */
+    MM_ERR_NOMEM = 5,       /* device allocation failed */
+    MM_ERR_UNSUPPORTED = 6
+};
+
+/* Flow kinds of the flow program (applied in declared order every step). */
+enum mm_flow_kind {
+    /* Exponencial from every cell of attribute a to its Moore neighbours:
+     * out = rate*v (src/Exponencial.hpp:18-20), share = out/count_neighbors
+     * (src/Model.hpp:199), v' = (v - out) + sum of neighbour shares
+     * (src/Model.hpp:206-211,234). The generalised whole-grid step. */
+    MM_FLOW_DIFFUSE = 1,
+    /* Exponencial from attribute a to attribute b of the SAME cell:
+     * out = rate*v_a; v_a -= out; v_b += out (b < 0: outflow leaves the system). */
+    MM_FLOW_TRANSFER = 2
+};
+
+enum mm_fill_mode {
+    MM_FILL_UNIFORM = 0,  /* v = value (the reference init is 1.0, src/Model.hpp:155) */
+    MM_FILL_RANDOM = 1    /* v = 1 + u(splitmix64(seed ^ (x*W+y))), global index keyed */
+};
+
+enum mm_halo_mode {
+    MM_HALO_NONE = 0,     /* single slab (nranks == 1) */
+    MM_HALO_RCCL = 1,     /* ncclSend/ncclRecv of border rows over xGMI, on a comm stream */
+    MM_HALO_HOST = 2      /* caller moves border rows (mm_halo_export / mm_halo_import) */
+};
+
+/* Engine description: one engine = one row slab of one grid on one GPU. */
+typedef struct mm_desc {
+    long long H, W;      /* global grid: DIMX rows x DIMY columns (src/Defines.hpp:5-6) */
+    long long x_init;    /* first global row owned by this slab (src/Model.hpp:72) */
+    long long h;         /* rows owned (src/Model.hpp:72 height) */
+    int n_attr;          /* attributes per cell, 1..4 (SoA fp64 buffers) */
+    int device;          /* HIP device ordinal */
+    int rank, nranks;    /* position in the 1-D chain of slabs (rank r-1 owns the rows above) */
+    int halo_mode;       /* enum mm_halo_mode */
+    const void* comm_id; /* MM_HALO_RCCL: mm_comm_id_size() bytes from mm_comm_id_create() on rank 0 */
+} mm_desc;
+
+typedef struct mm_engine mm_engine;
+
+/* Engine facts for measurement / debugging. */
+typedef struct mm_info {
+    long long pitch;           /* row pitch in doubles (>= W, multiple of 128) */
+    long long bytes_device;    /* device bytes held by the engine */
+    int n_passes;              /* kernel passes per step of the current flow program */
+    int rows_per_wave;         /* row block height of the step kernel */
+    long long waves_per_pass;  /* waves launched per pass */
+    long long steps_done;      /* steps run since the last fill/upload */
+    int fused_attrs;           /* attributes carried per fused pass */
+    int reserved;
+} mm_info;
+
+/* ---- host-only helpers (no GPU needed) ---------------------------------- */
+int mm_abi_version(void);
+const char* mm_last_error(void);
+
+/* src/Model.hpp:47-51 -- number of iterations of for(t=0; t<time; t+=time_step). */
+long long mm_step_count(double time, double time_step);
+
+/* src/Model.hpp:60-76 -- reference partition of worker k (1..P) of P = comm_size-1,
+ * int arithmetic exactly as the reference (remainder rows are dropped). */
+int mm_partition_reference(int H, int W, int P, int k,
+                           int* x_init, int* y_init, int* height, int* width);
+/* src/Model.hpp:80 -- rank owning global row x under the reference partition. */
+int mm_owner_reference(int H, int P, int x);
+/* Engine partition: slab g of G owns rows [floor(g*H/G), floor((g+1)*H/G)).
+ * Identical to mm_partition_reference(k = g+1) whenever G divides H. */
+int mm_partition_rows(long long H, int G, int g, long long* x_init, long long* h);
+/* src/Cell.hpp:71-157 -- Moore neighbour count of (x,y): 3 corner, 5 edge, 8 inside. */
+int mm_neighbor_count(long long H, long long W, long long x, long long y);
+
+/* RCCL bootstrap: rank 0 creates the id, every rank passes it in mm_desc.comm_id.
+ * Replaces the master's partition/flow descriptor messages (src/Model.hpp:70-86). */
+int mm_comm_id_size(void);
+int mm_comm_id_create(void* out, int len);
+
+int mm_device_count(int* n);
+
+/* ---- engine ------------------------------------------------------------- */
+/* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
+ * init loop (src/Model.hpp:154-157): device buffers are (h+2) x pitch fp64 per
+ * attribute (one ghost row above and below), two of them (Jacobi ping-pong). */
+int mm_engine_create(const mm_desc* desc, mm_engine** out);
+int mm_engine_destroy(mm_engine* eng);
+int mm_engine_info(mm_engine* eng, mm_info* info);
+
+/* src/Model.hpp:154-157 -- initialise one attribute on the device (owned and ghost rows). */
+int mm_fill(mm_engine* eng, int attr, int mode, double value, unsigned long long seed);
+/* Host <-> device copies of the OWNED rows (h x W, row-major, contiguous). */
+int mm_upload(mm_engine* eng, int attr, const double* host);
+int mm_download(mm_engine* eng, int attr, double* host);
+
+/* Flow program. src/Model.hpp:23-27 stores one Flow; the engine keeps an ordered list. */
+int mm_clear_flows(mm_engine* eng);
+int mm_add_flow(mm_engine* eng, int kind, int a, int b, double rate);
+
+/* src/Model.hpp:176-235 -- the reference's single-source Exponencial application:
+ * out = rate*captured (src/Exponencial.hpp:14-16, the Flow's own copy of the
+ * source value), share = out/count_neighbors to every in-grid Moore neighbour,
+ * source -= out. Applied in place to the cells this slab owns; no message needed
+ * (every slab computes the share from the same flow description). */
+int mm_point_apply(mm_engine* eng, int attr, long long sx, long long sy,
+                   double captured, double rate);
+
+/* Run nsteps steps of the flow program (the commented-out time loop,
+ * src/Model.hpp:180-183, made real). Every reduce_every-th step (0 = never) the
+ * per-attribute sums of the owned cells are reduced on the device and appended
+ * to the engine's history (src/Model.hpp:237-243 per-rank sum; MPI_Report).
+ * Asynchronous: returns once the work is enqueued. MM_HALO_HOST engines with
+ * nranks > 1 accept nsteps == 1 only (the caller exchanges between steps). */
+int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
+int mm_synchronize(mm_engine* eng);
+
+/* Sums of the owned cells. mm_sums reduces the CURRENT state now (synchronous).
+ * mm_sums_history copies up to max_entries recorded reductions (n_attr doubles
+ * each, oldest first) and returns the count in *n. */
+int mm_sums(mm_engine* eng, double* out_per_attr);
+int mm_sums_history(mm_engine* eng, double* out, long long max_entries, long long* n);
+int mm_clear_history(mm_engine* eng);
+
+/* MM_HALO_HOST transport: copy this slab's first/last owned rows of every
+ * attribute out (top/bottom: n_attr*W doubles each), and the neighbours' rows
+ * into the ghost rows (NULL = no neighbour on that side). Replaces the
+ * scalar halo messages src/Model.hpp:202-204 <-> :228-230 with whole rows. */
+int mm_halo_export(mm_engine* eng, double* top, double* bottom);
+int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
+
+/* Measurement: with timing on, mm_run records a HIP event pair around every
+ * step-kernel launch on the stream it is launched on; mm_timing returns the
+ * number of timed launches, their summed duration (ms) and the algorithmic
+ * bytes one launch moves (16 B per cell per attribute). */
+int mm_set_timing(mm_engine* eng, int on);
+int mm_timing(mm_engine* eng, long long* n_launches, double* total_ms, double* bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,749 @@
+// mm_engine.hip -- the host engine behind include/mpimodel.h (C ABI).
+//
+// One engine = one row slab of the global grid on one GPU:
+//   * device memory: per attribute two (h+2) x pitch fp64 buffers (Jacobi
+//     ping-pong), local row 0 / h+1 are ghost rows, pitch a multiple of 128;
+//   * a compute stream and a comm stream; with MM_HALO_RCCL each pass first
+//     exchanges border rows with ncclSend/ncclRecv on the comm stream while the
+//     interior rows run on the compute stream, then the two border rows run;
+//   * steps are captured once into a hipGraph (one ping-pong cycle, RCCL
+//     calls included) and replayed;
+//   * per-step sums (MPI_Report) are reduced on the device into a history.
+// The reference's per-worker body this replaces is src/Model.hpp:135-261.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mpimodel.h"
+#include "mm_internal.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define MM_HIP(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(MM_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));     \
+    } while (0)
+
+#define MM_NCCL(expr)                                                                     \
+    do {                                                                                  \
+        ncclResult_t r_ = (expr);                                                         \
+        if (r_ != ncclSuccess)                                                            \
+            return fail(MM_ERR_RCCL, std::string(#expr ": ") + ncclGetErrorString(r_));   \
+    } while (0)
+
+#define MM_TRY(expr)             \
+    do {                         \
+        int rc_ = (expr);        \
+        if (rc_ != MM_OK) return rc_; \
+    } while (0)
+
+long long span_rows(long long n, long long i) { return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0; }
+
+struct Transfer {
+    int a, b;
+    double rate;
+};
+
+// A fused pass: pre-chain transfers, at most one diffusion per attribute, post-chain.
+struct Pass {
+    std::vector<Transfer> pre, post;
+    int diffuse_mask = 0;
+    double drate[mm::kMaxAttr] = {0, 0, 0, 0};
+};
+
+struct FlowDesc {
+    int kind, a, b;
+    double rate;
+};
+
+}  // namespace
+
+struct mm_engine {
+    mm_desc d{};
+    int na = 1;
+    long long pitch = 0;
+    long long rows_alloc = 0;  // h + 2
+    double* base = nullptr;
+    size_t bytes = 0;
+    double* buf[2][mm::kMaxAttr] = {};
+    int cur = 0;
+    hipStream_t s_comp = nullptr, s_comm = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    ncclComm_t comm = nullptr;
+    bool split = false;  // interior / border split (RCCL halo)
+
+    std::vector<FlowDesc> flows;
+    std::vector<Pass> passes;
+
+    int th = 32;
+    int nstrips = 0;
+    double* partials = nullptr;
+    long long partials_cap = 0;
+    double* hist = nullptr;
+    unsigned long long* hist_n = nullptr;
+    long long hist_cap = 0;
+    double* sum_tmp = nullptr;  // mm_sums scratch: nblocks partials + 1 result per attribute
+    long long sum_blocks = 0;
+
+    long long steps_done = 0;
+
+    // graph cache: key = (parity, length, reduce_every)
+    std::map<std::tuple<int, long long, long long>, hipGraphExec_t> graphs;
+
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    long long timed_launches = 0;
+    double timed_ms = 0.0;
+};
+
+namespace {
+
+int set_device(mm_engine* e) {
+    MM_HIP(hipSetDevice(e->d.device));
+    return MM_OK;
+}
+
+void drop_graphs(mm_engine* e) {
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
+    e->graphs.clear();
+}
+
+int compile_passes(mm_engine* e) {
+    e->passes.clear();
+    Pass cur;
+    bool open = false;
+    for (const FlowDesc& f : e->flows) {
+        if (f.kind == MM_FLOW_TRANSFER) {
+            if (!open) {
+                cur = Pass();
+                open = true;
+            }
+            std::vector<Transfer>& chain = cur.diffuse_mask ? cur.post : cur.pre;
+            if ((int)chain.size() >= mm::kMaxChain) {
+                e->passes.push_back(cur);
+                cur = Pass();
+                cur.pre.push_back({f.a, f.b, f.rate});
+            } else {
+                chain.push_back({f.a, f.b, f.rate});
+            }
+        } else {  // MM_FLOW_DIFFUSE
+            if (!open) {
+                cur = Pass();
+                open = true;
+            }
+            if ((cur.diffuse_mask & (1 << f.a)) || !cur.post.empty()) {
+                e->passes.push_back(cur);
+                cur = Pass();
+            }
+            cur.diffuse_mask |= 1 << f.a;
+            cur.drate[f.a] = f.rate;
+        }
+    }
+    if (open) e->passes.push_back(cur);
+    return MM_OK;
+}
+
+// Waves for a row range of n rows.
+long long waves_for(const mm_engine* e, long long n) {
+    if (n <= 0) return 0;
+    return e->nstrips * ((n + e->th - 1) / e->th);
+}
+
+void fill_args(const mm_engine* e, const Pass& p, mm::PassArgs& A) {
+    std::memset(&A, 0, sizeof A);
+    for (int a = 0; a < e->na; ++a) {
+        A.in[a] = e->buf[e->cur][a];
+        A.out[a] = e->buf[e->cur ^ 1][a];
+    }
+    A.H = e->d.H;
+    A.W = e->d.W;
+    A.x_init = e->d.x_init;
+    A.pitch = e->pitch;
+    A.th = e->th;
+    A.nstrips = e->nstrips;
+    A.diffuse_mask = p.diffuse_mask;
+    for (int a = 0; a < mm::kMaxAttr; ++a) A.drate[a] = p.drate[a];
+    A.npre = (int)p.pre.size();
+    A.npost = (int)p.post.size();
+    for (size_t i = 0; i < p.pre.size(); ++i) {
+        A.pre_a[i] = (signed char)p.pre[i].a;
+        A.pre_b[i] = (signed char)p.pre[i].b;
+        A.pre_r[i] = p.pre[i].rate;
+    }
+    for (size_t i = 0; i < p.post.size(); ++i) {
+        A.post_a[i] = (signed char)p.post[i].a;
+        A.post_b[i] = (signed char)p.post[i].b;
+        A.post_r[i] = p.post[i].rate;
+    }
+    A.partials = e->partials;
+}
+
+hipEvent_t next_event(mm_engine* e) {
+    if (e->ev_used == e->ev_pool.size()) {
+        hipEvent_t ev;
+        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        e->ev_pool.push_back(ev);
+    }
+    return e->ev_pool[e->ev_used++];
+}
+
+int launch_timed(mm_engine* e, int na, bool reduce, const mm::PassArgs& A, bool time_it) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (time_it) {
+        a = next_event(e);
+        b = next_event(e);
+        if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
+        MM_HIP(hipEventRecord(a, e->s_comp));
+    }
+    MM_HIP(mm::launch_pass(na, reduce, A, e->s_comp));
+    if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
+    return MM_OK;
+}
+
+int halo_rccl(mm_engine* e) {
+    const int r = e->d.rank, n = e->d.nranks;
+    const long long W = e->d.W, P = e->pitch, h = e->d.h;
+    MM_NCCL(ncclGroupStart());
+    for (int a = 0; a < e->na; ++a) {
+        double* b = e->buf[e->cur][a];
+        if (r > 0) {
+            MM_NCCL(ncclSend(b + 1 * P, (size_t)W, ncclDouble, r - 1, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b + 0 * P, (size_t)W, ncclDouble, r - 1, e->comm, e->s_comm));
+        }
+        if (r < n - 1) {
+            MM_NCCL(ncclSend(b + h * P, (size_t)W, ncclDouble, r + 1, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b + (h + 1) * P, (size_t)W, ncclDouble, r + 1, e->comm, e->s_comm));
+        }
+    }
+    MM_NCCL(ncclGroupEnd());
+    return MM_OK;
+}
+
+// Enqueue one step (all passes). reduce: append the per-attribute sums to the history.
+int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
+    const long long h = e->d.h;
+    const int np = (int)e->passes.size();
+    for (int pi = 0; pi < np; ++pi) {
+        const Pass& p = e->passes[pi];
+        const bool red = reduce && pi == np - 1;
+        mm::PassArgs A;
+        fill_args(e, p, A);
+        if (e->split && h >= 3) {
+            MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
+            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
+            MM_TRY(halo_rccl(e));
+            MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
+            // interior rows 2..h-1 need no ghost row
+            A.ra0 = 2;
+            A.ra1 = (int)h;
+            A.rb0 = A.rb1 = 0;
+            A.waves_a = waves_for(e, h - 2);
+            A.waves_total = A.waves_a;
+            A.partial_base = 0;
+            MM_TRY(launch_timed(e, e->na, red, A, time_it));
+            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
+            // border rows 1 and h
+            const long long wa = A.waves_total;
+            A.ra0 = 1;
+            A.ra1 = 2;
+            A.rb0 = (int)h;
+            A.rb1 = (int)h + 1;
+            A.waves_a = waves_for(e, 1);
+            A.waves_total = 2 * A.waves_a;
+            A.partial_base = wa;
+            MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp));
+            if (red)
+                MM_HIP(mm::launch_finalize(e->partials, wa + A.waves_total, e->na, e->hist,
+                                           e->hist_n, e->hist_cap, e->s_comp));
+        } else {
+            if (e->split) {  // tiny slab (h < 3): exchange first, then one launch
+                MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
+                MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
+                MM_TRY(halo_rccl(e));
+                MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
+                MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
+            }
+            A.ra0 = 1;
+            A.ra1 = (int)h + 1;
+            A.rb0 = A.rb1 = 0;
+            A.waves_a = waves_for(e, h);
+            A.waves_total = A.waves_a;
+            A.partial_base = 0;
+            MM_TRY(launch_timed(e, e->na, red, A, time_it));
+            if (red)
+                MM_HIP(mm::launch_finalize(e->partials, A.waves_total, e->na, e->hist, e->hist_n,
+                                           e->hist_cap, e->s_comp));
+        }
+        e->cur ^= 1;
+    }
+    return MM_OK;
+}
+
+long long gcd_ll(long long a, long long b) {
+    while (b) {
+        long long t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_t* out) {
+    auto key = std::make_tuple(e->cur, len, reduce_every);
+    auto it = e->graphs.find(key);
+    if (it != e->graphs.end()) {
+        *out = it->second;
+        return MM_OK;
+    }
+    const int cur0 = e->cur;
+    MM_HIP(hipStreamBeginCapture(e->s_comp, hipStreamCaptureModeThreadLocal));
+    int rc = MM_OK;
+    for (long long i = 1; i <= len && rc == MM_OK; ++i)
+        rc = enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false);
+    hipGraph_t g = nullptr;
+    hipError_t ec = hipStreamEndCapture(e->s_comp, &g);
+    e->cur = cur0;  // capture only recorded the work; the state advances at replay
+    if (rc != MM_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (ec != hipSuccess) return fail(MM_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+    hipGraphExec_t ge = nullptr;
+    ec = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ec != hipSuccess) return fail(MM_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ec));
+    e->graphs[key] = ge;
+    *out = ge;
+    return MM_OK;
+}
+
+int choose_th(const mm_engine* e) {
+    if (const char* s = std::getenv("MM_ROWS_PER_WAVE")) {
+        int v = std::atoi(s);
+        if (v >= 1) return v;
+    }
+    // aim for ~4096 waves (16 per CU on 256 CUs), rows per wave in [16, 512]
+    const long long target = 4096;
+    long long th = (e->d.h * (long long)e->nstrips + target - 1) / target;
+    th = std::max<long long>(16, std::min<long long>(512, th));
+    return (int)th;
+}
+
+int ensure_partials(mm_engine* e) {
+    long long need = waves_for(e, e->d.h) + 2 * waves_for(e, 1) + 16;
+    if (need <= e->partials_cap) return MM_OK;
+    if (e->partials) (void)hipFree(e->partials);
+    e->partials = nullptr;
+    MM_HIP(hipMalloc(&e->partials, sizeof(double) * (size_t)need * mm::kMaxAttr));
+    e->partials_cap = need;
+    return MM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mm_abi_version(void) { return MM_ABI_VERSION; }
+
+const char* mm_last_error(void) { return g_last_error.c_str(); }
+
+long long mm_step_count(double time, double time_step) {
+    if (!(time_step > 0.0)) return -1;  // the reference would loop forever
+    long long n = 0;
+    for (double t = 0; t < time; t = t + time_step) ++n;  // src/Model.hpp:48, same fp64 sequence
+    return n;
+}
+
+int mm_partition_reference(int H, int W, int P, int k, int* x_init, int* y_init, int* height,
+                           int* width) {
+    if (H <= 0 || W <= 0 || P <= 0 || k < 1 || k > P || !x_init || !y_init || !height || !width)
+        return fail(MM_ERR_INVALID, "mm_partition_reference: bad arguments");
+    const int count = (H * W) / P;  // src/Model.hpp:63
+    const int offset = (k - 1) * count;
+    *x_init = offset / W;  // src/Model.hpp:72
+    *y_init = 0;
+    *height = H / P;
+    *width = W;
+    return MM_OK;
+}
+
+int mm_owner_reference(int H, int P, int x) {
+    if (H <= 0 || P <= 0 || H / P == 0) return -1;
+    return x / (H / P) + 1;  // src/Model.hpp:80
+}
+
+int mm_partition_rows(long long H, int G, int g, long long* x_init, long long* h) {
+    if (H <= 0 || G <= 0 || g < 0 || g >= G || !x_init || !h)
+        return fail(MM_ERR_INVALID, "mm_partition_rows: bad arguments");
+    const long long a = (g * H) / G, b = ((g + 1) * H) / G;
+    *x_init = a;
+    *h = b - a;
+    return MM_OK;
+}
+
+int mm_neighbor_count(long long H, long long W, long long x, long long y) {
+    const long long sx = span_rows(H, x), sy = span_rows(W, y);
+    return (sx && sy) ? (int)(sx * sy - 1) : 0;
+}
+
+int mm_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int mm_comm_id_create(void* out, int len) {
+    if (!out || len < (int)sizeof(ncclUniqueId)) return fail(MM_ERR_INVALID, "mm_comm_id_create: buffer too small");
+    ncclUniqueId id;
+    MM_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof id);
+    return MM_OK;
+}
+
+int mm_device_count(int* n) {
+    if (!n) return fail(MM_ERR_INVALID, "mm_device_count: null");
+    MM_HIP(hipGetDeviceCount(n));
+    return MM_OK;
+}
+
+int mm_engine_create(const mm_desc* desc, mm_engine** out) {
+    if (!desc || !out) return fail(MM_ERR_INVALID, "mm_engine_create: null argument");
+    *out = nullptr;
+    const mm_desc& d = *desc;
+    if (d.H <= 0 || d.W <= 0 || d.h <= 0 || d.x_init < 0 || d.x_init + d.h > d.H)
+        return fail(MM_ERR_INVALID, "mm_engine_create: slab outside the grid");
+    if (d.n_attr < 1 || d.n_attr > mm::kMaxAttr)
+        return fail(MM_ERR_INVALID, "mm_engine_create: n_attr must be 1..4");
+    if (d.nranks < 1 || d.rank < 0 || d.rank >= d.nranks)
+        return fail(MM_ERR_INVALID, "mm_engine_create: bad rank/nranks");
+    if (d.nranks == 1 && (d.x_init != 0 || d.h != d.H))
+        return fail(MM_ERR_INVALID, "mm_engine_create: a single slab must own the whole grid");
+    if (d.halo_mode == MM_HALO_RCCL && d.nranks > 1 && !d.comm_id)
+        return fail(MM_ERR_INVALID, "mm_engine_create: MM_HALO_RCCL needs comm_id");
+    if (d.nranks > 1 && d.halo_mode == MM_HALO_NONE)
+        return fail(MM_ERR_INVALID, "mm_engine_create: nranks > 1 needs a halo mode");
+    if (d.W > (1LL << 30) || d.h > (1LL << 30))
+        return fail(MM_ERR_INVALID, "mm_engine_create: slab too large");
+
+    mm_engine* e = new mm_engine();
+    e->d = d;
+    e->na = d.n_attr;
+    e->pitch = (d.W + mm::kStripCols - 1) / mm::kStripCols * mm::kStripCols;
+    e->nstrips = (int)(e->pitch / mm::kStripCols);
+    e->rows_alloc = d.h + 2;
+    e->th = choose_th(e);
+
+    auto cleanup = [&](int rc) {
+        mm_engine_destroy(e);
+        return rc;
+    };
+    hipError_t he = hipSetDevice(d.device);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
+
+    const size_t per = (size_t)e->rows_alloc * (size_t)e->pitch;  // doubles per buffer
+    const size_t per_al = (per + 31) / 32 * 32;                   // 256-B aligned buffers
+    e->bytes = sizeof(double) * per_al * 2 * (size_t)e->na;
+    he = hipMalloc(&e->base, e->bytes);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he)));
+    he = hipMemset(e->base, 0, e->bytes);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(he)));
+    for (int k = 0; k < 2; ++k)
+        for (int a = 0; a < e->na; ++a) e->buf[k][a] = e->base + per_al * (size_t)(k * e->na + a);
+
+    if (hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_halo, hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(MM_ERR_HIP, "stream/event creation failed"));
+
+    int rc = ensure_partials(e);
+    if (rc != MM_OK) return cleanup(rc);
+    e->hist_cap = 1 << 16;
+    if (hipMalloc(&e->hist, sizeof(double) * (size_t)e->hist_cap * e->na) != hipSuccess ||
+        hipMalloc(&e->hist_n, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->hist_n, 0, sizeof(unsigned long long)) != hipSuccess)
+        return cleanup(fail(MM_ERR_NOMEM, "history allocation failed"));
+    e->sum_blocks = std::min<long long>(1024, std::max<long long>(1, d.h));
+    if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)
+        return cleanup(fail(MM_ERR_NOMEM, "sum scratch allocation failed"));
+
+    if (d.nranks > 1 && d.halo_mode == MM_HALO_RCCL) {
+        ncclUniqueId id;
+        std::memcpy(&id, d.comm_id, sizeof id);
+        ncclResult_t nr = ncclCommInitRank(&e->comm, d.nranks, id, d.rank);
+        if (nr != ncclSuccess)
+            return cleanup(fail(MM_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr)));
+        e->split = true;
+    }
+    // default program: one Exponencial flow on attribute 0 is set by the caller
+    *out = e;
+    return MM_OK;
+}
+
+int mm_engine_destroy(mm_engine* e) {
+    if (!e) return MM_OK;
+    (void)hipSetDevice(e->d.device);
+    if (e->s_comp) (void)hipStreamSynchronize(e->s_comp);
+    if (e->s_comm) (void)hipStreamSynchronize(e->s_comm);
+    drop_graphs(e);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
+    if (e->ev_halo) (void)hipEventDestroy(e->ev_halo);
+    if (e->s_comp) (void)hipStreamDestroy(e->s_comp);
+    if (e->s_comm) (void)hipStreamDestroy(e->s_comm);
+    if (e->base) (void)hipFree(e->base);
+    if (e->partials) (void)hipFree(e->partials);
+    if (e->hist) (void)hipFree(e->hist);
+    if (e->hist_n) (void)hipFree(e->hist_n);
+    if (e->sum_tmp) (void)hipFree(e->sum_tmp);
+    delete e;
+    return MM_OK;
+}
+
+int mm_engine_info(mm_engine* e, mm_info* info) {
+    if (!e || !info) return fail(MM_ERR_INVALID, "mm_engine_info: null");
+    std::memset(info, 0, sizeof *info);
+    info->pitch = e->pitch;
+    info->bytes_device = (long long)e->bytes;
+    info->n_passes = (int)e->passes.size();
+    info->rows_per_wave = e->th;
+    info->waves_per_pass = waves_for(e, e->d.h);
+    info->steps_done = e->steps_done;
+    info->fused_attrs = e->na;
+    return MM_OK;
+}
+
+int mm_fill(mm_engine* e, int attr, int mode, double value, unsigned long long seed) {
+    if (!e || attr < 0 || attr >= e->na || (mode != MM_FILL_UNIFORM && mode != MM_FILL_RANDOM))
+        return fail(MM_ERR_INVALID, "mm_fill: bad arguments");
+    MM_TRY(set_device(e));
+    MM_HIP(mm::launch_fill(e->buf[e->cur][attr], e->pitch, e->d.H, e->d.W, e->d.x_init, e->d.h,
+                           mode, value, seed, e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    e->steps_done = 0;
+    return MM_OK;
+}
+
+int mm_upload(mm_engine* e, int attr, const double* host) {
+    if (!e || !host || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_upload: bad arguments");
+    MM_TRY(set_device(e));
+    MM_HIP(hipMemcpy2DAsync(e->buf[e->cur][attr] + e->pitch, sizeof(double) * e->pitch, host,
+                            sizeof(double) * e->d.W, sizeof(double) * e->d.W, e->d.h,
+                            hipMemcpyHostToDevice, e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    e->steps_done = 0;
+    return MM_OK;
+}
+
+int mm_download(mm_engine* e, int attr, double* host) {
+    if (!e || !host || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_download: bad arguments");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    MM_HIP(hipMemcpy2DAsync(host, sizeof(double) * e->d.W, e->buf[e->cur][attr] + e->pitch,
+                            sizeof(double) * e->pitch, sizeof(double) * e->d.W, e->d.h,
+                            hipMemcpyDeviceToHost, e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_clear_flows(mm_engine* e) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_clear_flows: null");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    e->flows.clear();
+    e->passes.clear();
+    drop_graphs(e);
+    return MM_OK;
+}
+
+int mm_add_flow(mm_engine* e, int kind, int a, int b, double rate) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_add_flow: null");
+    if (kind != MM_FLOW_DIFFUSE && kind != MM_FLOW_TRANSFER)
+        return fail(MM_ERR_INVALID, "mm_add_flow: unknown flow kind");
+    if (a < 0 || a >= e->na) return fail(MM_ERR_INVALID, "mm_add_flow: attribute out of range");
+    if (kind == MM_FLOW_TRANSFER && b >= e->na)
+        return fail(MM_ERR_INVALID, "mm_add_flow: target attribute out of range");
+    if (!std::isfinite(rate)) return fail(MM_ERR_INVALID, "mm_add_flow: rate must be finite");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    e->flows.push_back({kind, a, kind == MM_FLOW_TRANSFER ? (b < 0 ? -1 : b) : a, rate});
+    drop_graphs(e);
+    return compile_passes(e);
+}
+
+int mm_point_apply(mm_engine* e, int attr, long long sx, long long sy, double captured,
+                   double rate) {
+    if (!e || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_point_apply: bad arguments");
+    if (sx < 0 || sy < 0 || sx >= e->d.H || sy >= e->d.W)
+        return fail(MM_ERR_INVALID, "mm_point_apply: source cell outside the grid");
+    MM_TRY(set_device(e));
+    MM_HIP(mm::launch_point(e->buf[e->cur][attr], e->pitch, e->d.H, e->d.W, e->d.x_init, e->d.h,
+                            sx, sy, captured, rate, e->s_comp));
+    return MM_OK;
+}
+
+int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
+    if (!e || nsteps < 0 || reduce_every < 0) return fail(MM_ERR_INVALID, "mm_run: bad arguments");
+    if (nsteps == 0) return MM_OK;
+    if (e->passes.empty()) return fail(MM_ERR_STATE, "mm_run: no flow added (mm_add_flow)");
+    if (e->d.halo_mode == MM_HALO_HOST && e->d.nranks > 1) {
+        if (nsteps != 1 || e->passes.size() != 1)
+            return fail(MM_ERR_STATE, "mm_run: host halo transport runs one single-pass step per call");
+    }
+    MM_TRY(set_device(e));
+    const int np = (int)e->passes.size();
+    if (e->timing) {  // eager launches with an event pair around each step kernel
+        for (long long i = 1; i <= nsteps; ++i)
+            MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, true));
+        e->steps_done += nsteps;
+        return MM_OK;
+    }
+    // graph of one ping-pong cycle (and of the reduction period), replayed
+    const long long cycle = (np % 2) ? 2 : 1;
+    long long len = cycle;
+    if (reduce_every > 0) len = cycle / gcd_ll(cycle, reduce_every) * reduce_every;
+    if (len > 256 || nsteps < len) {
+        for (long long i = 1; i <= nsteps; ++i)
+            MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false));
+        e->steps_done += nsteps;
+        return MM_OK;
+    }
+    // replay graph chunks of `len` steps; at least a few steps per replay
+    long long per = len;
+    while (per < 8 && per * 2 <= nsteps) per *= 2;
+    hipGraphExec_t g = nullptr;
+    MM_TRY(get_graph(e, per, reduce_every, &g));
+    long long done = 0;
+    for (; done + per <= nsteps; done += per) {
+        MM_HIP(hipGraphLaunch(g, e->s_comp));
+        if ((np * per) % 2) e->cur ^= 1;
+        // the graph was captured for a fixed parity: re-fetch if it flipped
+        if ((np * per) % 2) MM_TRY(get_graph(e, per, reduce_every, &g));
+    }
+    for (long long i = done + 1; i <= nsteps; ++i)
+        MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false));
+    e->steps_done += nsteps;
+    return MM_OK;
+}
+
+int mm_synchronize(mm_engine* e) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_synchronize: null");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    return MM_OK;
+}
+
+int mm_sums(mm_engine* e, double* out) {
+    if (!e || !out) return fail(MM_ERR_INVALID, "mm_sums: null");
+    MM_TRY(set_device(e));
+    for (int a = 0; a < e->na; ++a)
+        MM_HIP(mm::launch_slab_sum(e->buf[e->cur][a], e->pitch, e->d.W, e->d.h, e->sum_tmp,
+                                   e->sum_blocks, e->sum_tmp + e->sum_blocks + a, e->s_comp));
+    MM_HIP(hipMemcpyAsync(out, e->sum_tmp + e->sum_blocks, sizeof(double) * e->na,
+                          hipMemcpyDeviceToHost, e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_sums_history(mm_engine* e, double* out, long long max_entries, long long* n) {
+    if (!e || !n || (max_entries > 0 && !out)) return fail(MM_ERR_INVALID, "mm_sums_history: bad arguments");
+    MM_TRY(set_device(e));
+    unsigned long long cnt = 0;
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    MM_HIP(hipMemcpy(&cnt, e->hist_n, sizeof cnt, hipMemcpyDeviceToHost));
+    long long avail = std::min<long long>((long long)cnt, e->hist_cap);
+    long long k = std::min(avail, max_entries);
+    if (k > 0) MM_HIP(hipMemcpy(out, e->hist, sizeof(double) * (size_t)(k * e->na), hipMemcpyDeviceToHost));
+    *n = (long long)cnt;
+    return MM_OK;
+}
+
+int mm_clear_history(mm_engine* e) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_clear_history: null");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    MM_HIP(hipMemset(e->hist_n, 0, sizeof(unsigned long long)));
+    return MM_OK;
+}
+
+int mm_halo_export(mm_engine* e, double* top, double* bottom) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_halo_export: null");
+    MM_TRY(set_device(e));
+    const long long W = e->d.W, P = e->pitch, h = e->d.h;
+    for (int a = 0; a < e->na; ++a) {
+        if (top)
+            MM_HIP(hipMemcpyAsync(top + a * W, e->buf[e->cur][a] + 1 * P, sizeof(double) * W,
+                                  hipMemcpyDeviceToHost, e->s_comp));
+        if (bottom)
+            MM_HIP(hipMemcpyAsync(bottom + a * W, e->buf[e->cur][a] + h * P, sizeof(double) * W,
+                                  hipMemcpyDeviceToHost, e->s_comp));
+    }
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_halo_import(mm_engine* e, const double* top, const double* bottom) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_halo_import: null");
+    MM_TRY(set_device(e));
+    const long long W = e->d.W, P = e->pitch, h = e->d.h;
+    for (int a = 0; a < e->na; ++a) {
+        if (top)
+            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + 0 * P, top + a * W, sizeof(double) * W,
+                                  hipMemcpyHostToDevice, e->s_comp));
+        if (bottom)
+            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + (h + 1) * P, bottom + a * W,
+                                  sizeof(double) * W, hipMemcpyHostToDevice, e->s_comp));
+    }
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_set_timing(mm_engine* e, int on) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_set_timing: null");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    e->timing = on != 0;
+    e->ev_used = 0;
+    e->timed_launches = 0;
+    e->timed_ms = 0.0;
+    return MM_OK;
+}
+
+int mm_timing(mm_engine* e, long long* n, double* total_ms, double* bytes_per_launch) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_timing: null");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    for (size_t i = 0; i + 1 < e->ev_used; i += 2) {
+        float ms = 0.f;
+        MM_HIP(hipEventElapsedTime(&ms, e->ev_pool[i], e->ev_pool[i + 1]));
+        e->timed_ms += ms;
+        e->timed_launches += 1;
+    }
+    e->ev_used = 0;
+    if (n) *n = e->timed_launches;
+    if (total_ms) *total_ms = e->timed_ms;
+    if (bytes_per_launch) {
+        // algorithmic bytes of one full-slab launch: read + write 8 B per cell per attribute
+        int moved = 0;
+        if (!e->passes.empty()) moved = e->na;
+        *bytes_per_launch = 16.0 * (double)e->d.h * (double)e->d.W * moved;
+    }
+    return MM_OK;
+}
+
+}  // extern "C"

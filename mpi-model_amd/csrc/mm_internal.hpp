@@ -1,0 +1,56 @@
+// mm_internal.hpp -- shared between the gfx950 kernels (mm_kernels.hip) and the
+// engine / C ABI (mm_engine.hip). Not part of the public boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace mm {
+
+constexpr int kMaxAttr = 4;     // SoA attributes per fused pass (config C5: 4)
+constexpr int kMaxChain = 8;    // elementwise transfers before / after a pass's diffusion
+constexpr int kStripCols = 128; // columns per wave: 64 lanes x double2 (16 B per lane)
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = 64 * kWavesPerBlock;
+
+// One fused Jacobi pass over a row slab (every buffer is (h+2) x pitch fp64,
+// local row 0 / h+1 are the ghost rows, local row r is global row x_init+r-1):
+//   u  = pre-chain transfers applied to the loaded cell values
+//   per diffusing attribute a: out = rate_a*u, s = out/cnt, w = (u - out) + nb(s)
+//   w  = post-chain transfers applied to w;  store w
+// Rows [ra0, ra1) and [rb0, rb1) (local, half-open) are computed; the second
+// range lets one launch cover both border rows of a halo-split step.
+struct PassArgs {
+    const double* in[kMaxAttr];
+    double* out[kMaxAttr];
+    long long H, W, x_init, pitch;
+    int ra0, ra1, rb0, rb1;
+    int th;                 // rows per wave
+    int nstrips;            // column strips of 128 per row
+    long long waves_a;      // waves covering range a
+    long long waves_total;  // waves covering both ranges
+    int diffuse_mask;       // bit a: attribute a diffuses in this pass
+    int npre, npost;
+    double drate[kMaxAttr];
+    signed char pre_a[kMaxChain], pre_b[kMaxChain];
+    signed char post_a[kMaxChain], post_b[kMaxChain];
+    double pre_r[kMaxChain], post_r[kMaxChain];
+    double* partials;       // REDUCE: [partial_base + wave][NA]
+    long long partial_base;
+};
+
+// Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
+hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s);
+hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
+                       long long h, int mode, double value, unsigned long long seed, hipStream_t s);
+hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,
+                        long long h, long long sx, long long sy, double captured, double rate,
+                        hipStream_t s);
+// Sum partials[n][na] in a fixed order into hist[k][na], k = (*hist_n)++ (device
+// counter, so the launch is graph-replayable); entries beyond cap are dropped.
+hipError_t launch_finalize(const double* partials, long long n, int na, double* hist,
+                           unsigned long long* hist_n, long long cap, hipStream_t s);
+// Per-attribute sum of the owned rows of one buffer (no pass), into out[0].
+hipError_t launch_slab_sum(const double* buf, long long pitch, long long W, long long h,
+                           double* partials, long long nblocks, double* out_sum, hipStream_t s);
+
+}  // namespace mm

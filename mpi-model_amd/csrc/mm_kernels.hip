@@ -1,0 +1,469 @@
+// mm_kernels.hip -- gfx950 kernels for the MPI-Model flow step.
+//
+// Hot path: mm_pass_kernel, the whole-grid Exponencial step (the
+// generalisation of src/Model.hpp:176-235 + src/Exponencial.hpp:18-20 to every
+// cell and every step). It is HBM-bound (about 11 fp64 flop per 16 B), so the
+// design is all about streaming:
+//   * one wave owns a strip of 128 columns x th rows; lane l holds columns
+//     2l, 2l+1 and moves them as one 16-B double2 (1 KiB per wave-instruction,
+//     fully coalesced row-major loads and stores);
+//   * the wave slides DOWN its strip keeping three rows of shares s in
+//     registers, so the x-1 / x+1 neighbours cost no memory traffic;
+//   * the y-1 / y+1 neighbours come from the adjacent lanes through DPP
+//     wave_shr:1 / wave_shl:1 (no LDS, no barrier); lanes 0 and 63 additionally
+//     load the one column left / right of the strip;
+//   * rows are prefetched U at a time so every wave keeps U KiB in flight.
+// Arithmetic order is the contract in oracle/mm_oracle.h; the .so is built with
+// -ffp-contract=off so no multiply/add pair is fused.
+#include "mm_internal.hpp"
+
+namespace mm {
+
+namespace {
+
+__device__ __forceinline__ double dpp_from_lower_lane(double src, double old) {
+    // lane i <- lane i-1 (wave_shr:1); lane 0 keeps `old`
+    const long long s = __double_as_longlong(src), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double dpp_from_upper_lane(double src, double old) {
+    // lane i <- lane i+1 (wave_shl:1); lane 63 keeps `old`
+    const long long s = __double_as_longlong(src), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), 0x130, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// 1 + (i > 0) + (i < n-1) inside [0, n), 0 outside: cnt = span(x)*span(y) - 1
+__device__ __forceinline__ int span3(long long n, long long i) {
+    return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
+}
+
+// share of one emitter (src/Model.hpp:199); cnt == 8 as the exact *0.125
+__device__ __forceinline__ double share_of(double out, int cnt) {
+    return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
+}
+
+template <int NA>
+__device__ __forceinline__ void apply_chain(double (&u)[NA], int n, const signed char* ta,
+                                            const signed char* tb, const double* tr) {
+    for (int t = 0; t < n; ++t) {
+        const int a = ta[t], b = tb[t];
+        const double r = tr[t];
+        double src = 0.0;
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (k == a) src = u[k];
+        const double out = r * src;
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (k == a) u[k] = u[k] - out;
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (k == b) u[k] = u[k] + out;
+    }
+}
+
+// Raw values of one row as this lane sees them: its two columns + its edge column.
+template <int NA>
+struct RawRow {
+    double v0[NA], v1[NA], ve[NA];
+};
+
+// Processed row: shares (three columns) and u - out (two columns).
+template <int NA>
+struct ProcRow {
+    double s0[NA], s1[NA], se[NA];
+    double d0[NA], d1[NA];
+};
+
+template <int NA>
+__device__ __forceinline__ void load_row(const PassArgs& A, int r, long long y0, long long ye,
+                                         bool edge_ok, RawRow<NA>& o) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        const double* row = A.in[a] + (long long)r * A.pitch;
+        const double2 p = *reinterpret_cast<const double2*>(row + y0);
+        o.v0[a] = p.x;
+        o.v1[a] = p.y;
+        o.ve[a] = edge_ok ? row[ye] : 0.0;
+    }
+}
+
+template <int NA>
+__device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawRow<NA>& raw,
+                                            bool fast_cols, int sy0, int sy1, int sye,
+                                            ProcRow<NA>& o) {
+    const long long gx = A.x_init + r - 1;
+    const int sx = span3(A.H, gx);
+    double u0[NA], u1[NA], ue[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        u0[a] = raw.v0[a];
+        u1[a] = raw.v1[a];
+        ue[a] = raw.ve[a];
+    }
+    if (A.npre) {
+        apply_chain<NA>(u0, A.npre, A.pre_a, A.pre_b, A.pre_r);
+        apply_chain<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
+        apply_chain<NA>(ue, A.npre, A.pre_a, A.pre_b, A.pre_r);
+    }
+    if (sx == 0) {  // row outside the global grid: emits nothing
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            o.s0[a] = o.s1[a] = o.se[a] = 0.0;
+            o.d0[a] = u0[a];
+            o.d1[a] = u1[a];
+        }
+        return;
+    }
+    if (sx == 3 && fast_cols) {  // interior rows and columns: cnt == 8 everywhere
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            if (A.diffuse_mask & (1 << a)) {
+                const double r_ = A.drate[a];
+                const double o0 = r_ * u0[a], o1 = r_ * u1[a], oe = r_ * ue[a];
+                o.s0[a] = o0 * 0.125;
+                o.s1[a] = o1 * 0.125;
+                o.se[a] = oe * 0.125;
+                o.d0[a] = u0[a] - o0;
+                o.d1[a] = u1[a] - o1;
+            } else {
+                o.s0[a] = o.s1[a] = o.se[a] = 0.0;
+                o.d0[a] = u0[a];
+                o.d1[a] = u1[a];
+            }
+        }
+        return;
+    }
+    const int c0 = (sx && sy0) ? sx * sy0 - 1 : 0;
+    const int c1 = (sx && sy1) ? sx * sy1 - 1 : 0;
+    const int ce = (sx && sye) ? sx * sye - 1 : 0;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        if (A.diffuse_mask & (1 << a)) {
+            const double r_ = A.drate[a];
+            const double o0 = c0 > 0 ? r_ * u0[a] : 0.0;
+            const double o1 = c1 > 0 ? r_ * u1[a] : 0.0;
+            const double oe = ce > 0 ? r_ * ue[a] : 0.0;
+            o.s0[a] = share_of(o0, c0);
+            o.s1[a] = share_of(o1, c1);
+            o.se[a] = share_of(oe, ce);
+            o.d0[a] = u0[a] - o0;
+            o.d1[a] = u1[a] - o1;
+        } else {
+            o.s0[a] = o.s1[a] = o.se[a] = 0.0;
+            o.d0[a] = u0[a];
+            o.d1[a] = u1[a];
+        }
+    }
+}
+
+template <int NA, bool REDUCE>
+__device__ __forceinline__ void emit_row(const PassArgs& A, int r, long long y0, bool st2,
+                                         bool st1, const ProcRow<NA>& P, const ProcRow<NA>& C,
+                                         const ProcRow<NA>& N, double (&acc)[NA]) {
+    double w0[NA], w1[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        if (A.diffuse_mask & (1 << a)) {
+            const double p0 = P.s0[a] + N.s0[a];
+            const double p1 = P.s1[a] + N.s1[a];
+            const double pe = P.se[a] + N.se[a];
+            const double c0 = p0 + C.s0[a];
+            const double c1 = p1 + C.s1[a];
+            const double ce = pe + C.se[a];
+            const double left = dpp_from_lower_lane(c1, ce);   // c3 at column y0-1
+            const double right = dpp_from_upper_lane(c0, ce);  // c3 at column y0+2
+            w0[a] = C.d0[a] + ((left + c1) + p0);
+            w1[a] = C.d1[a] + ((c0 + right) + p1);
+        } else {
+            w0[a] = C.d0[a];
+            w1[a] = C.d1[a];
+        }
+    }
+    if (A.npost) {
+        apply_chain<NA>(w0, A.npost, A.post_a, A.post_b, A.post_r);
+        apply_chain<NA>(w1, A.npost, A.post_a, A.post_b, A.post_r);
+    }
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        double* row = A.out[a] + (long long)r * A.pitch;
+        if (st2) {
+            *reinterpret_cast<double2*>(row + y0) = make_double2(w0[a], w1[a]);
+        } else if (st1) {
+            row[y0] = w0[a];
+        }
+        if (REDUCE) {
+            if (st1) acc[a] = acc[a] + w0[a];
+            if (st2) acc[a] = acc[a] + w1[a];
+        }
+    }
+}
+
+template <int NA>
+__device__ __forceinline__ void copy_row(ProcRow<NA>& d, const ProcRow<NA>& s) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        d.s0[a] = s.s0[a];
+        d.s1[a] = s.s1[a];
+        d.se[a] = s.se[a];
+        d.d0[a] = s.d0[a];
+        d.d1[a] = s.d1[a];
+    }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+    // fixed butterfly: every lane ends with the same, order-independent-of-timing value
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
+    return v;
+}
+
+template <int NA, int U, bool REDUCE>
+__global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
+    const int lane = threadIdx.x & 63;
+    const long long wid =
+        (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);  // wave-uniform
+    if (wid >= A.waves_total) return;
+
+    // wave -> (row range, row block, column strip); strips vary fastest so the 4 waves of
+    // a block are side by side and share their edge columns in L1/L2.
+    int rlo, rhi;
+    long long w = wid;
+    if (w < A.waves_a) {
+        rlo = A.ra0;
+        rhi = A.ra1;
+    } else {
+        w -= A.waves_a;
+        rlo = A.rb0;
+        rhi = A.rb1;
+    }
+    const int strip = (int)(w % A.nstrips);
+    const int rb = (int)(w / A.nstrips);
+    const int rA = rlo + rb * A.th;
+    const int rB = min(rA + A.th, rhi);
+
+    const long long base = (long long)strip * kStripCols;
+    const long long y0 = base + 2 * lane;
+    const long long W = A.W;
+    // lane 0 carries the column left of the strip, lane 63 the one right of it
+    const long long ye = lane == 0 ? base - 1 : (lane == 63 ? base + kStripCols : -1);
+    const bool edge_ok = ye >= 0 && ye < W;
+    const int sy0 = span3(W, y0), sy1 = span3(W, y0 + 1), sye = edge_ok ? span3(W, ye) : 0;
+    const bool fast_cols = base >= 2 && base + kStripCols <= W - 2;  // wave-uniform
+    const bool st1 = y0 < W, st2 = y0 + 1 < W;
+
+    double acc[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+
+    ProcRow<NA> P, C, N;
+    {
+        RawRow<NA> r0, r1;
+        load_row<NA>(A, rA - 1, y0, ye, edge_ok, r0);
+        load_row<NA>(A, rA, y0, ye, edge_ok, r1);
+        process_row<NA>(A, rA - 1, r0, fast_cols, sy0, sy1, sye, P);
+        process_row<NA>(A, rA, r1, fast_cols, sy0, sy1, sye, C);
+    }
+    for (int r = rA; r < rB; r += U) {
+        RawRow<NA> raw[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) load_row<NA>(A, min(r + 1 + k, rB), y0, ye, edge_ok, raw[k]);
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (r + k >= rB) break;
+            process_row<NA>(A, r + 1 + k, raw[k], fast_cols, sy0, sy1, sye, N);
+            emit_row<NA, REDUCE>(A, r + k, y0, st2, st1, P, C, N, acc);
+            copy_row<NA>(P, C);
+            copy_row<NA>(C, N);
+        }
+    }
+
+    if (REDUCE) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const double t = wave_sum(acc[a]);
+            if (lane == 0) A.partials[(A.partial_base + wid) * NA + a] = t;
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// src/Model.hpp:154-157 (value 1.0) or the synthetic input of SURVEY.md 8(d);
+// owned rows and the ghost rows that lie inside the grid.
+__global__ __launch_bounds__(256) void mm_fill_kernel(double* buf, long long pitch, long long H,
+                                                      long long W, long long x_init, long long h,
+                                                      int mode, double value,
+                                                      unsigned long long seed) {
+    const long long n = (h + 2) * W;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / W, y = i - r * W;
+        const long long gx = x_init + r - 1;
+        if (gx < 0 || gx >= H) continue;
+        double v = value;
+        if (mode == 1) {
+            const unsigned long long z = splitmix64(seed ^ (unsigned long long)(gx * W + y));
+            v = 1.0 + (double)(z >> 11) * 0x1.0p-53;
+        }
+        buf[r * pitch + y] = v;
+    }
+}
+
+// src/Model.hpp:176-235 on the cells of this slab (one thread per 3x3 cell).
+__global__ void mm_point_kernel(double* buf, long long pitch, long long H, long long W,
+                                long long x_init, long long h, long long sx, long long sy,
+                                double captured, double rate) {
+    const int t = threadIdx.x;
+    if (t >= 9) return;
+    const int cnt = (span3(H, sx) && span3(W, sy)) ? span3(H, sx) * span3(W, sy) - 1 : 0;
+    if (cnt <= 0) return;
+    const long long x = sx + t / 3 - 1, y = sy + t % 3 - 1;
+    if (x < 0 || y < 0 || x >= H || y >= W || x < x_init || x >= x_init + h) return;
+    const double out = rate * captured;        // src/Exponencial.hpp:15
+    const double share = share_of(out, cnt);   // src/Model.hpp:199
+    double* p = buf + (x - x_init + 1) * pitch + y;
+    if (t == 4)
+        *p = *p - out;    // src/Model.hpp:211
+    else
+        *p = *p + share;  // src/Model.hpp:206-209,234
+}
+
+// Fixed-order sum of n partial rows (na doubles each) -> hist[k], k from a device counter.
+__global__ __launch_bounds__(256) void mm_finalize_kernel(const double* partials, long long n,
+                                                          int na, double* hist,
+                                                          unsigned long long* hist_n,
+                                                          long long cap) {
+    __shared__ double red[256];
+    __shared__ unsigned long long slot;
+    if (threadIdx.x == 0) slot = *hist_n;
+    __syncthreads();
+    for (int a = 0; a < na; ++a) {
+        double s = 0.0;
+        for (long long i = threadIdx.x; i < n; i += 256) s = s + partials[i * na + a];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int m = 128; m >= 1; m >>= 1) {
+            if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0 && (long long)slot < cap) hist[slot * na + a] = red[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *hist_n = slot + 1;
+}
+
+// Sum of the owned rows of one buffer: block b sums rows b, b+nblocks, ...
+__global__ __launch_bounds__(256) void mm_slab_sum_kernel(const double* buf, long long pitch,
+                                                          long long W, long long h,
+                                                          double* partials) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (long long r = blockIdx.x; r < h; r += gridDim.x) {
+        const double* row = buf + (r + 1) * pitch;
+        for (long long y = threadIdx.x; y < W; y += 256) s = s + row[y];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int m = 128; m >= 1; m >>= 1) {
+        if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+__global__ void mm_sum_partials_kernel(const double* partials, long long n, double* out) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (long long i = threadIdx.x; i < n; i += 256) s = s + partials[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int m = 128; m >= 1; m >>= 1) {
+        if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// rows kept in flight per wave: 8 KiB per wave at one attribute, fewer rows as the
+// attributes (and the registers per row) grow
+template <int NA>
+constexpr int prefetch_rows() {
+    return NA == 1 ? 8 : (NA == 2 ? 4 : 2);
+}
+
+template <int NA>
+hipError_t launch_pass_na(bool reduce, const PassArgs& a, hipStream_t s) {
+    const long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
+    constexpr int U = prefetch_rows<NA>();
+    if (reduce)
+        hipLaunchKernelGGL((mm_pass_kernel<NA, U, true>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                           s, a);
+    else
+        hipLaunchKernelGGL((mm_pass_kernel<NA, U, false>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                           s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s) {
+    if (a.waves_total <= 0) return hipSuccess;
+    switch (na) {
+        case 1: return launch_pass_na<1>(reduce, a, s);
+        case 2: return launch_pass_na<2>(reduce, a, s);
+        case 3: return launch_pass_na<3>(reduce, a, s);
+        case 4: return launch_pass_na<4>(reduce, a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
+                       long long h, int mode, double value, unsigned long long seed,
+                       hipStream_t s) {
+    const long long n = (h + 2) * W;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(mm_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, pitch, H, W,
+                       x_init, h, mode, value, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,
+                        long long h, long long sx, long long sy, double captured, double rate,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(mm_point_kernel, dim3(1), dim3(64), 0, s, buf, pitch, H, W, x_init, h, sx,
+                       sy, captured, rate);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const double* partials, long long n, int na, double* hist,
+                           unsigned long long* hist_n, long long cap, hipStream_t s) {
+    hipLaunchKernelGGL(mm_finalize_kernel, dim3(1), dim3(256), 0, s, partials, n, na, hist, hist_n,
+                       cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_slab_sum(const double* buf, long long pitch, long long W, long long h,
+                           double* partials, long long nblocks, double* out_sum, hipStream_t s) {
+    hipLaunchKernelGGL(mm_slab_sum_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, buf, pitch, W,
+                       h, partials);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mm_sum_partials_kernel, dim3(1), dim3(256), 0, s, partials, nblocks,
+                       out_sum);
+    return hipGetLastError();
+}
+
+}  // namespace mm

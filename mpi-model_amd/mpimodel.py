@@ -1,0 +1,260 @@
+"""ctypes binding of the C ABI in include/mpimodel.h (libmpimodel_hip.so).
+
+Host-side mirror of the reference's Model/CellularSpace/Exponencial interface for
+Python callers (bench.py, tests). The C++ mirror for Main.cpp-style programs is
+mpi-model_amd/api/. There is no fallback: if the HIP library is missing or no
+GPU is visible, these calls raise -- nothing here computes on the CPU.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmpimodel_hip.so")
+
+MM_OK = 0
+MM_FLOW_DIFFUSE = 1
+MM_FLOW_TRANSFER = 2
+MM_FILL_UNIFORM = 0
+MM_FILL_RANDOM = 1
+MM_HALO_NONE = 0
+MM_HALO_RCCL = 1
+MM_HALO_HOST = 2
+SEED = 0x4D50494D
+
+# every symbol include/mpimodel.h declares
+EXPORTS = [
+    "mm_abi_version", "mm_last_error", "mm_step_count", "mm_partition_reference",
+    "mm_owner_reference", "mm_partition_rows", "mm_neighbor_count", "mm_comm_id_size",
+    "mm_comm_id_create", "mm_device_count", "mm_engine_create", "mm_engine_destroy",
+    "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
+    "mm_point_apply", "mm_run", "mm_synchronize", "mm_sums", "mm_sums_history",
+    "mm_clear_history", "mm_halo_export", "mm_halo_import", "mm_set_timing", "mm_timing",
+]
+
+
+class MMError(RuntimeError):
+    """Non-zero mm_status; the C++ API raises std::runtime_error the same way
+    (reference convention: src/MPIImpl.cpp:7-8,13-14)."""
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_longlong), ("W", ctypes.c_longlong),
+                ("x_init", ctypes.c_longlong), ("h", ctypes.c_longlong),
+                ("n_attr", ctypes.c_int), ("device", ctypes.c_int),
+                ("rank", ctypes.c_int), ("nranks", ctypes.c_int),
+                ("halo_mode", ctypes.c_int), ("comm_id", ctypes.c_void_p)]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [("pitch", ctypes.c_longlong), ("bytes_device", ctypes.c_longlong),
+                ("n_passes", ctypes.c_int), ("rows_per_wave", ctypes.c_int),
+                ("waves_per_pass", ctypes.c_longlong), ("steps_done", ctypes.c_longlong),
+                ("fused_attrs", ctypes.c_int), ("reserved", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MMError(f"{LIB_PATH} not built: run `make -C mpi-model_amd` "
+                          "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        LL, D, I, P = ctypes.c_longlong, ctypes.c_double, ctypes.c_int, ctypes.c_void_p
+        pLL, pI = ctypes.POINTER(LL), ctypes.POINTER(I)
+        sig = {
+            "mm_abi_version": (I, []),
+            "mm_last_error": (ctypes.c_char_p, []),
+            "mm_step_count": (LL, [D, D]),
+            "mm_partition_reference": (I, [I, I, I, I, pI, pI, pI, pI]),
+            "mm_owner_reference": (I, [I, I, I]),
+            "mm_partition_rows": (I, [LL, I, I, pLL, pLL]),
+            "mm_neighbor_count": (I, [LL, LL, LL, LL]),
+            "mm_comm_id_size": (I, []),
+            "mm_comm_id_create": (I, [P, I]),
+            "mm_device_count": (I, [pI]),
+            "mm_engine_create": (I, [ctypes.POINTER(Desc), ctypes.POINTER(P)]),
+            "mm_engine_destroy": (I, [P]),
+            "mm_engine_info": (I, [P, ctypes.POINTER(Info)]),
+            "mm_fill": (I, [P, I, I, D, ctypes.c_ulonglong]),
+            "mm_upload": (I, [P, I, P]),
+            "mm_download": (I, [P, I, P]),
+            "mm_clear_flows": (I, [P]),
+            "mm_add_flow": (I, [P, I, I, I, D]),
+            "mm_point_apply": (I, [P, I, LL, LL, D, D]),
+            "mm_run": (I, [P, LL, LL]),
+            "mm_synchronize": (I, [P]),
+            "mm_sums": (I, [P, P]),
+            "mm_sums_history": (I, [P, P, LL, pLL]),
+            "mm_clear_history": (I, [P]),
+            "mm_halo_export": (I, [P, P, P]),
+            "mm_halo_import": (I, [P, P, P]),
+            "mm_set_timing": (I, [P, I]),
+            "mm_timing": (I, [P, pLL, ctypes.POINTER(D), ctypes.POINTER(D)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != MM_OK:
+        raise MMError(f"mm error {rc}: {lib().mm_last_error().decode(errors='replace')}")
+
+
+def _dptr(a):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---- host-only bookkeeping (src/Model.hpp:47-80, src/Cell.hpp:71-157) ----------
+def step_count(time, time_step):
+    return lib().mm_step_count(time, time_step)
+
+
+def partition_reference(H, W, P, k):
+    o = [ctypes.c_int() for _ in range(4)]
+    check(lib().mm_partition_reference(H, W, P, k, *[ctypes.byref(x) for x in o]))
+    return tuple(x.value for x in o)
+
+
+def owner_reference(H, P, x):
+    return lib().mm_owner_reference(H, P, x)
+
+
+def partition_rows(H, G, g):
+    a, h = ctypes.c_longlong(), ctypes.c_longlong()
+    check(lib().mm_partition_rows(H, G, g, ctypes.byref(a), ctypes.byref(h)))
+    return a.value, h.value
+
+
+def neighbor_count(H, W, x, y):
+    return lib().mm_neighbor_count(H, W, x, y)
+
+
+def comm_id():
+    n = lib().mm_comm_id_size()
+    buf = ctypes.create_string_buffer(n)
+    check(lib().mm_comm_id_create(buf, n))
+    return buf.raw
+
+
+def device_count():
+    n = ctypes.c_int()
+    check(lib().mm_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Engine:
+    """One row slab [x_init, x_init+h) of an H x W grid on one GPU."""
+
+    def __init__(self, H, W, x_init=0, h=None, n_attr=1, device=0, rank=0, nranks=1,
+                 halo_mode=MM_HALO_NONE, comm_id_bytes=None):
+        h = H if h is None else h
+        self._id = None
+        if comm_id_bytes is not None:
+            self._id = ctypes.create_string_buffer(comm_id_bytes, len(comm_id_bytes))
+        d = Desc(H, W, x_init, h, n_attr, device, rank, nranks, halo_mode,
+                 ctypes.cast(self._id, ctypes.c_void_p) if self._id is not None else None)
+        p = ctypes.c_void_p()
+        check(lib().mm_engine_create(ctypes.byref(d), ctypes.byref(p)))
+        self.ptr = p
+        self.H, self.W, self.x_init, self.h, self.n_attr = H, W, x_init, h, n_attr
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            check(lib().mm_engine_destroy(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def info(self):
+        i = Info()
+        check(lib().mm_engine_info(self.ptr, ctypes.byref(i)))
+        return {k: getattr(i, k) for k, _ in Info._fields_}
+
+    def fill(self, attr=0, mode=MM_FILL_UNIFORM, value=1.0, seed=SEED):
+        check(lib().mm_fill(self.ptr, attr, mode, value, seed))
+
+    def fill_random(self, attr=0, seed=SEED):
+        self.fill(attr, MM_FILL_RANDOM, 0.0, seed)
+
+    def upload(self, host, attr=0):
+        a = np.ascontiguousarray(host, dtype=np.float64)
+        assert a.shape == (self.h, self.W)
+        check(lib().mm_upload(self.ptr, attr, _dptr(a)))
+
+    def download(self, attr=0):
+        out = np.empty((self.h, self.W), dtype=np.float64)
+        check(lib().mm_download(self.ptr, attr, _dptr(out)))
+        return out
+
+    def clear_flows(self):
+        check(lib().mm_clear_flows(self.ptr))
+
+    def add_diffuse(self, attr, rate):
+        check(lib().mm_add_flow(self.ptr, MM_FLOW_DIFFUSE, attr, attr, rate))
+
+    def add_transfer(self, a, b, rate):
+        check(lib().mm_add_flow(self.ptr, MM_FLOW_TRANSFER, a, b, rate))
+
+    def point_apply(self, sx, sy, captured, rate, attr=0):
+        check(lib().mm_point_apply(self.ptr, attr, sx, sy, captured, rate))
+
+    def run(self, nsteps, reduce_every=0):
+        check(lib().mm_run(self.ptr, nsteps, reduce_every))
+
+    def synchronize(self):
+        check(lib().mm_synchronize(self.ptr))
+
+    def sums(self):
+        out = np.empty(self.n_attr, dtype=np.float64)
+        check(lib().mm_sums(self.ptr, _dptr(out)))
+        return out
+
+    def sums_history(self, max_entries=1 << 16):
+        out = np.empty((max_entries, self.n_attr), dtype=np.float64)
+        n = ctypes.c_longlong()
+        check(lib().mm_sums_history(self.ptr, _dptr(out), max_entries, ctypes.byref(n)))
+        return out[:min(n.value, max_entries)].copy()
+
+    def clear_history(self):
+        check(lib().mm_clear_history(self.ptr))
+
+    def halo_export(self):
+        top = np.empty(self.n_attr * self.W, dtype=np.float64)
+        bot = np.empty(self.n_attr * self.W, dtype=np.float64)
+        check(lib().mm_halo_export(self.ptr, _dptr(top), _dptr(bot)))
+        return top, bot
+
+    def halo_import(self, top=None, bottom=None):
+        t = None if top is None else np.ascontiguousarray(top, dtype=np.float64)
+        b = None if bottom is None else np.ascontiguousarray(bottom, dtype=np.float64)
+        check(lib().mm_halo_import(self.ptr, _dptr(t), _dptr(b)))
+
+    def set_timing(self, on):
+        check(lib().mm_set_timing(self.ptr, 1 if on else 0))
+
+    def timing(self):
+        n, ms, b = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+        check(lib().mm_timing(self.ptr, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(b)))
+        return n.value, ms.value, b.value

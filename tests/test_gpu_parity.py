@@ -1,0 +1,239 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit for bit.
+
+Bar (BASELINE.json north_star): bit-exact cell indexing and partition bookkeeping;
+attribute values within 1e-12 relative (fp64). The step's arithmetic order is
+shared with the oracle (oracle/mm_oracle.h), so values are compared BIT-EXACTLY
+here; only sums (whose summation order differs by design) use the 1e-12 bound.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import golden, golden_points
+
+pytestmark = pytest.mark.gpu
+
+RATE = 0.1  # src/Main.cpp:33
+
+SHAPES = [(1, 1), (1, 9), (2, 2), (3, 5), (5, 3), (37, 53), (100, 100), (64, 128), (63, 129),
+          (130, 257), (257, 300), (33, 1000)]
+
+
+def run_field(gpu, v, rate, steps, reduce_every=0):
+    H, W = v.shape
+    with gpu.Engine(H, W) as e:
+        e.upload(v)
+        e.add_diffuse(0, rate)
+        e.run(steps, reduce_every)
+        e.synchronize()
+        return e.download(), (e.sums_history() if reduce_every else None)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_one_step_bit_exact(gpu, O, shape):
+    v = O.fill_random(*shape)
+    got, _ = run_field(gpu, v, RATE, 1)
+    assert np.array_equal(got, O.field_step(v, RATE))
+
+
+@pytest.mark.parametrize("shape,steps", [((37, 53), 2), ((100, 100), 7), ((130, 257), 10),
+                                          ((64, 128), 51)])
+def test_multi_step_bit_exact(gpu, O, shape, steps):
+    v = O.fill_random(*shape)
+    got, _ = run_field(gpu, v, 0.25, steps)
+    assert np.array_equal(got, O.field_step(v, 0.25, steps=steps))
+
+
+def test_device_fill_matches_oracle_input(gpu, O):
+    H, W = 77, 300
+    with gpu.Engine(H, W) as e:
+        e.fill_random(0)
+        assert np.array_equal(e.download(), O.fill_random(H, W))
+        e.fill(0, value=1.0)
+        assert np.array_equal(e.download(), np.ones((H, W)))
+
+
+@pytest.mark.parametrize("name", golden_points())
+def test_point_flow_matches_reference_golden(gpu, name):
+    # src/Model.hpp:176-235 on the device, against the grid the reference itself wrote
+    g = golden(name)
+    H, W = g["dimx"], g["dimy"]
+    with gpu.Engine(H, W) as e:
+        e.fill(0, value=1.0)
+        e.point_apply(g["src_x"], g["src_y"], float.fromhex(g["value_hex"]),
+                      float.fromhex(g["rate_hex"]))
+        v = e.download()
+        s = e.sums()[0]
+    changed = sorted([x, y, val.hex()] for (x, y), val in np.ndenumerate(v) if val != 1.0)
+    assert changed == g["changed"]
+    want = float.fromhex(g["sum_fsum_hex"])
+    assert abs(s - want) <= 1e-12 * abs(want)
+    assert s - H * W < 0.001  # the reference's own check, src/Model.hpp:95
+
+
+@pytest.mark.parametrize("name", golden_points())
+def test_point_flow_on_reference_partition(gpu, name):
+    # the same golden grid computed by P slabs laid out exactly as the reference's
+    # workers (src/Model.hpp:70-76), each applying the flow to the cells it owns
+    g = golden(name)
+    H, W, P = g["dimx"], g["dimy"], g["nworkers"]
+    parts = []
+    for k in range(1, P + 1):
+        x0, _, hh, _ = gpu.partition_reference(H, W, P, k)
+        assert (x0, hh) == gpu.partition_rows(H, P, k - 1)
+        with gpu.Engine(H, W, x0, hh, rank=k - 1, nranks=P, halo_mode=gpu.MM_HALO_HOST) as e:
+            e.fill(0, value=1.0)
+            e.point_apply(g["src_x"], g["src_y"], float.fromhex(g["value_hex"]),
+                          float.fromhex(g["rate_hex"]))
+            parts.append(e.download())
+    v = np.vstack(parts)
+    changed = sorted([x, y, val.hex()] for (x, y), val in np.ndenumerate(v) if val != 1.0)
+    assert changed == g["changed"]
+
+
+@pytest.mark.parametrize("H,W,G,steps", [(37, 53, 2, 3), (100, 100, 5, 4), (41, 300, 8, 2),
+                                         (9, 130, 3, 5)])
+def test_slabs_with_host_halo_bit_exact(gpu, O, H, W, G, steps):
+    v = O.fill_random(H, W)
+    engines = []
+    for g in range(G):
+        x0, h = gpu.partition_rows(H, G, g)
+        e = gpu.Engine(H, W, x0, h, rank=g, nranks=G, halo_mode=gpu.MM_HALO_HOST)
+        e.fill_random(0)
+        e.add_diffuse(0, RATE)
+        engines.append(e)
+    for _ in range(steps):
+        halos = [e.halo_export() for e in engines]
+        for g, e in enumerate(engines):
+            top = halos[g - 1][1] if g > 0 else None
+            bot = halos[g + 1][0] if g < G - 1 else None
+            e.halo_import(top, bot)
+        for e in engines:
+            e.run(1)
+    got = np.vstack([e.download() for e in engines])
+    for e in engines:
+        e.close()
+    assert np.array_equal(got, O.field_step(v, RATE, steps=steps))
+
+
+def test_step_sums_history(gpu, O):
+    H, W, steps = 130, 257, 6
+    v = O.fill_random(H, W)
+    got, hist = run_field(gpu, v, RATE, steps, reduce_every=1)
+    assert hist.shape == (steps, 1)
+    ref = v
+    for k in range(steps):
+        ref = O.field_step(ref, RATE)
+        want = math.fsum(ref.ravel())
+        assert abs(hist[k, 0] - want) <= 1e-12 * want
+    assert np.array_equal(got, ref)
+
+
+def test_sums_every_third_step(gpu, O):
+    v = O.fill_random(64, 128)
+    _, hist = run_field(gpu, v, RATE, 9, reduce_every=3)
+    assert hist.shape == (3, 1)
+    ref = v
+    for k in range(9):
+        ref = O.field_step(ref, RATE)
+        if (k + 1) % 3 == 0:
+            want = math.fsum(ref.ravel())
+            assert abs(hist[(k + 1) // 3 - 1, 0] - want) <= 1e-12 * want
+
+
+def test_timed_eager_path_equals_graph_path(gpu, O):
+    H, W = 257, 300
+    with gpu.Engine(H, W) as a, gpu.Engine(H, W) as b:
+        for e in (a, b):
+            e.fill_random(0)
+            e.add_diffuse(0, RATE)
+        a.set_timing(True)
+        a.run(20)
+        b.run(20)
+        n, ms, bytes_per = a.timing()
+        assert n == 20 and ms > 0 and bytes_per == 16.0 * H * W
+        assert np.array_equal(a.download(), b.download())
+
+
+C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
+            (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+
+
+def add_flows(e, flows):
+    for kind, a, b, r in flows:
+        if kind == 1:
+            e.add_diffuse(a, r)
+        else:
+            e.add_transfer(a, b, r)
+
+
+@pytest.mark.parametrize("flows,n_attr", [
+    (C5_FLOWS, 4),
+    ([(1, 0, 0, 0.1), (2, 0, 1, 0.2), (1, 1, 1, 0.3)], 2),       # post-chain, then a 2nd pass
+    ([(2, 0, -1, 0.01), (1, 0, 0, 0.1), (1, 0, 0, 0.2)], 1),      # sink, two diffusions of a
+    ([(2, 2, 0, 0.5), (1, 1, 1, 0.1), (2, 1, 2, 0.1)], 3),
+])
+def test_flow_program_bit_exact(gpu, O, flows, n_attr):
+    H, W, steps = 67, 300, 4
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(n_attr)]
+    want, sums = O.program_step(fields, flows, steps=steps, sums_per_step=True)
+    with gpu.Engine(H, W, n_attr=n_attr) as e:
+        for a in range(n_attr):
+            e.fill_random(a, seed=O.SEED + a)
+        add_flows(e, flows)
+        e.run(steps, reduce_every=1)
+        got = [e.download(a) for a in range(n_attr)]
+        hist = e.sums_history()
+    for a in range(n_attr):
+        assert np.array_equal(got[a], want[a]), a
+    assert hist.shape == (steps, n_attr)
+    for k in range(steps):
+        for a in range(n_attr):
+            w = sums[k][a]
+            assert abs(hist[k, a] - w) <= 1e-12 * abs(w), (k, a)
+
+
+def test_large_grid_properties(gpu, O):
+    # full-size checks via size-independent properties: conservation and exact
+    # mirror symmetry of the 4096^2 (config C2 shape) step, plus a row block
+    # compared with the oracle
+    H = W = 4096
+    steps = 20
+    with gpu.Engine(H, W) as e:
+        e.fill_random(0)
+        s0 = e.sums()[0]
+        e.add_diffuse(0, RATE)
+        e.run(steps)
+        v = e.download()
+        s1 = e.sums()[0]
+    assert abs(s1 - s0) <= 1e-12 * s0
+    v0 = O.fill_random(H, W)
+    assert abs(math.fsum(v0.ravel()) - s0) <= 1e-12 * s0
+    with gpu.Engine(H, W) as e:
+        e.upload(v0[::-1, ::-1].copy())
+        e.add_diffuse(0, RATE)
+        e.run(steps)
+        vf = e.download()
+    assert np.array_equal(vf, v[::-1, ::-1])
+
+
+def test_uniform_field_interior_fixed_point(gpu):
+    with gpu.Engine(512, 640) as e:
+        e.fill(0, value=1.0)
+        e.add_diffuse(0, 0.25)
+        e.run(10)
+        v = e.download()
+    assert np.all(v[11:-11, 11:-11] == 1.0)
+
+
+def test_engine_rejects_bad_shapes(gpu):
+    with pytest.raises(gpu.MMError):
+        gpu.Engine(10, 10, x_init=5, h=6, nranks=2, rank=1, halo_mode=gpu.MM_HALO_HOST)
+    with pytest.raises(gpu.MMError):
+        gpu.Engine(10, 10, n_attr=5)
+    with gpu.Engine(8, 8) as e:
+        with pytest.raises(gpu.MMError):
+            e.run(1)  # no flow
+        with pytest.raises(gpu.MMError):
+            e.point_apply(8, 0, 1.0, 0.1)

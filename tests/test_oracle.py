@@ -1,0 +1,126 @@
+"""CPU tests: the oracle against the reference's golden grids, and its invariants.
+
+The reference (daviidsilvaa/MPI-Model) has no tests of its own;
+its only built-in check is the conservation assert src/Model.hpp:95. These tests
+pin the C restatement (oracle/mm_oracle.c) to fixtures produced by the reference
+itself (tests/golden/make_golden.py), then check the generalised step's invariants.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import golden, golden_points
+
+
+@pytest.mark.parametrize("name", golden_points())
+def test_point_apply_matches_reference_golden(O, name):
+    g = golden(name)
+    H, W = g["dimx"], g["dimy"]
+    v = np.ones((H, W))
+    v = O.point_apply(v, g["src_x"], g["src_y"], float.fromhex(g["value_hex"]),
+                      float.fromhex(g["rate_hex"]))
+    changed = sorted([x, y, val.hex()] for (x, y), val in np.ndenumerate(v) if val != 1.0)
+    assert changed == g["changed"]
+    assert math.fsum(v.ravel()).hex() == g["sum_fsum_hex"]
+
+
+def test_default_golden_values_section0(O):
+    # source 0.78, its 8 neighbours 1.0275 (3 of them via halo)
+    g = golden("point_100_100_5_0.json")
+    vals = {(x, y): float.fromhex(h) for x, y, h in g["changed"]}
+    assert vals[(19, 3)].hex() == "0x1.8f5c28f5c28f6p-1"
+    for c in [(18, 2), (18, 3), (18, 4), (19, 2), (19, 4), (20, 2), (20, 3), (20, 4)]:
+        assert vals[c].hex() == "0x1.070a3d70a3d71p+0"
+
+
+@pytest.mark.parametrize("name", golden_points())
+def test_general_step_with_point_outflow_is_reference_update(O, name):
+    # the generalised step with outflow zero everywhere but the source IS the
+    # reference's single-source update (src/Model.hpp:176-235), bit for bit
+    g = golden(name)
+    H, W = g["dimx"], g["dimy"]
+    v = np.ones((H, W))
+    outf = np.zeros((H, W))
+    outf[g["src_x"], g["src_y"]] = float.fromhex(g["rate_hex"]) * float.fromhex(g["value_hex"])
+    o = O.field_step_general(v, outf)
+    assert np.array_equal(o, O.point_apply(v, g["src_x"], g["src_y"],
+                                           float.fromhex(g["value_hex"]),
+                                           float.fromhex(g["rate_hex"])))
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 7), (2, 2), (3, 5), (37, 53), (64, 130)])
+def test_uniform_rate_step_equals_general_form(O, shape):
+    H, W = shape
+    v = O.fill_random(H, W)
+    # a cell without neighbours (1x1 grid) cannot emit: its outflow is 0
+    emits = np.array([[O.neighbor_count(H, W, x, y) > 0 for y in range(W)] for x in range(H)])
+    outf = np.where(emits, 0.1 * v, 0.0)
+    assert np.array_equal(O.field_step(v, 0.1), O.field_step_general(v, outf))
+
+
+def test_step_count_matches_reference_loop(O):
+    # fp64 accumulation of src/Model.hpp:48
+    assert O.step_count(10.0, 0.2) == 51
+    assert O.step_count(1.0, 0.1) == 11
+    assert O.step_count(100.0, 0.1) == 1001
+    assert O.step_count(1000.0, 1.0) == 1000
+
+
+def test_neighbor_counts_match_cell_hpp(O):
+    # src/Cell.hpp:71-157: corners 3, edges 5, interior 8 (grids >= 2x2)
+    for H, W in [(2, 2), (3, 3), (100, 100), (5, 9)]:
+        for x in range(H):
+            for y in range(W):
+                corner = x in (0, H - 1) and y in (0, W - 1)
+                edge = (x in (0, H - 1) or y in (0, W - 1)) and not corner
+                want = 3 if corner else (5 if edge else 8)
+                if H == 2 or W == 2:  # 2-wide grids: no interior, edges as in Cell.hpp
+                    want = 3 if corner else 5
+                assert O.neighbor_count(H, W, x, y) == want
+
+
+def test_conservation_and_uniform_fixed_point(O):
+    v = O.fill_random(61, 47)
+    o = O.field_step(v, 0.1, steps=20)
+    s0, s1 = math.fsum(v.ravel()), math.fsum(o.ravel())
+    assert abs(s1 - s0) <= 1e-12 * abs(s0)
+    u = O.field_step(np.ones((20, 30)), 0.25, steps=5)
+    # cells farther than steps+1 from the edge receive exactly what they emit
+    # (rate 0.25: every share 1/32 is exact)
+    assert np.all(u[6:-6, 6:-6] == 1.0)
+    assert not np.all(u == 1.0)
+
+
+def test_flip_symmetry_is_exact(O):
+    v = O.fill_random(33, 45)
+    a = O.field_step(v, 0.25, steps=3)
+    assert np.array_equal(O.field_step(v[::-1].copy(), 0.25, steps=3), a[::-1])
+    assert np.array_equal(O.field_step(v[:, ::-1].copy(), 0.25, steps=3), a[:, ::-1])
+
+
+@pytest.mark.parametrize("H,G", [(37, 1), (37, 2), (37, 3), (40, 4), (41, 8), (9, 9)])
+def test_slab_decomposition_is_bit_exact(O, H, G):
+    W = 29
+    v = O.fill_random(H, W)
+    want = O.field_step(v, 0.1)
+    parts = []
+    for g in range(G):
+        x0, h = O.partition_rows(H, G, g)
+        vg = np.zeros((h + 2, W))
+        lo, hi = max(x0 - 1, 0), min(x0 + h + 1, H)
+        vg[lo - (x0 - 1):hi - (x0 - 1)] = v[lo:hi]
+        parts.append(O.field_step_slab(H, W, x0, vg, 0.1))
+    assert np.array_equal(np.vstack(parts), want)
+
+
+def test_program_step_conserves_total(O):
+    H, W = 24, 40
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    flows = [(O.TRANSFER, 0, 1, 0.05), (O.TRANSFER, 1, 2, 0.03), (O.TRANSFER, 2, 3, 0.02),
+             (O.TRANSFER, 3, 0, 0.01), (O.DIFFUSE, 0, 0, 0.1), (O.DIFFUSE, 1, 1, 0.1),
+             (O.DIFFUSE, 2, 2, 0.05), (O.DIFFUSE, 3, 3, 0.2)]
+    out = O.program_step(fields, flows, steps=10)
+    t0 = math.fsum(np.concatenate([f.ravel() for f in fields]))
+    t1 = math.fsum(np.concatenate([f.ravel() for f in out]))
+    assert abs(t1 - t0) <= 1e-12 * t0
