@@ -92,6 +92,7 @@ struct mm_engine {
     std::vector<Pass> passes;
 
     int th = 32;
+    int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
     double* partials = nullptr;
     long long partials_cap = 0;
@@ -212,7 +213,7 @@ int launch_timed(mm_engine* e, int na, bool reduce, const mm::PassArgs& A, bool 
         if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
         MM_HIP(hipEventRecord(a, e->s_comp));
     }
-    MM_HIP(mm::launch_pass(na, reduce, A, e->s_comp));
+    MM_HIP(mm::launch_pass(na, reduce, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
     return MM_OK;
 }
@@ -268,7 +269,7 @@ int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
             A.waves_a = waves_for(e, 1);
             A.waves_total = 2 * A.waves_a;
             A.partial_base = wa;
-            MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp));
+            MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
             if (red)
                 MM_HIP(mm::launch_finalize(e->partials, wa + A.waves_total, e->na, e->hist,
                                            e->hist_n, e->hist_cap, e->s_comp));
@@ -445,6 +446,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->nstrips = (int)(e->pitch / mm::kStripCols);
     e->rows_alloc = d.h + 2;
     e->th = choose_th(e);
+    if (const char* v = std::getenv("MM_KERNEL_VARIANT")) e->variant = std::atoi(v);
 
     auto cleanup = [&](int rc) {
         mm_engine_destroy(e);

@@ -39,7 +39,7 @@ struct PassArgs {
 };
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
-hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s);
+hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
                        long long h, int mode, double value, unsigned long long seed, hipStream_t s);
 hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,

@@ -80,13 +80,20 @@ struct ProcRow {
     double d0[NA], d1[NA];
 };
 
-template <int NA>
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+// NT bit 1: non-temporal loads; bit 0: non-temporal stores
+template <int NA, int NT>
 __device__ __forceinline__ void load_row(const PassArgs& A, int r, long long y0, long long ye,
                                          bool edge_ok, RawRow<NA>& o) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         const double* row = A.in[a] + (long long)r * A.pitch;
-        const double2 p = *reinterpret_cast<const double2*>(row + y0);
+        dv2 p;
+        if (NT & 2)
+            p = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(row + y0));
+        else
+            p = *reinterpret_cast<const dv2*>(row + y0);
         o.v0[a] = p.x;
         o.v1[a] = p.y;
         o.ve[a] = edge_ok ? row[ye] : 0.0;
@@ -162,7 +169,7 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
     }
 }
 
-template <int NA, bool REDUCE>
+template <int NA, bool REDUCE, int NT>
 __device__ __forceinline__ void emit_row(const PassArgs& A, int r, long long y0, bool st2,
                                          bool st1, const ProcRow<NA>& P, const ProcRow<NA>& C,
                                          const ProcRow<NA>& N, double (&acc)[NA]) {
@@ -193,7 +200,13 @@ __device__ __forceinline__ void emit_row(const PassArgs& A, int r, long long y0,
     for (int a = 0; a < NA; ++a) {
         double* row = A.out[a] + (long long)r * A.pitch;
         if (st2) {
-            *reinterpret_cast<double2*>(row + y0) = make_double2(w0[a], w1[a]);
+            dv2 v;
+            v.x = w0[a];
+            v.y = w1[a];
+            if (NT & 1)
+                __builtin_nontemporal_store(v, reinterpret_cast<dv2*>(row + y0));
+            else
+                *reinterpret_cast<dv2*>(row + y0) = v;
         } else if (st1) {
             row[y0] = w0[a];
         }
@@ -223,7 +236,7 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-template <int NA, int U, bool REDUCE>
+template <int NA, int U, bool REDUCE, int NT>
 __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
     const int lane = threadIdx.x & 63;
     const long long wid =
@@ -261,23 +274,25 @@ __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) acc[a] = 0.0;
 
-    ProcRow<NA> P, C, N;
-    {
-        RawRow<NA> r0, r1;
-        load_row<NA>(A, rA - 1, y0, ye, edge_ok, r0);
-        load_row<NA>(A, rA, y0, ye, edge_ok, r1);
-        process_row<NA>(A, rA - 1, r0, fast_cols, sy0, sy1, sye, P);
-        process_row<NA>(A, rA, r1, fast_cols, sy0, sy1, sye, C);
-    }
-    for (int r = rA; r < rB; r += U) {
-        RawRow<NA> raw[U];
+    // Rolling prefetch: raw[k] holds input row r+1+k of the current group of U output
+    // rows; right after row r+k is emitted, raw[k] is refilled with row r+1+k+U, so U
+    // row loads stay in flight for the whole strip.
+    RawRow<NA> first, second, raw[U];
+    load_row<NA, NT>(A, rA - 1, y0, ye, edge_ok, first);
+    load_row<NA, NT>(A, rA, y0, ye, edge_ok, second);
 #pragma unroll
-        for (int k = 0; k < U; ++k) load_row<NA>(A, min(r + 1 + k, rB), y0, ye, edge_ok, raw[k]);
+    for (int k = 0; k < U; ++k)
+        if (rA + 1 + k <= rB) load_row<NA, NT>(A, rA + 1 + k, y0, ye, edge_ok, raw[k]);
+    ProcRow<NA> P, C, N;
+    process_row<NA>(A, rA - 1, first, fast_cols, sy0, sy1, sye, P);
+    process_row<NA>(A, rA, second, fast_cols, sy0, sy1, sye, C);
+    for (int r = rA; r < rB; r += U) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            if (r + k >= rB) break;
+            if (r + k >= rB) break;  // wave-uniform
             process_row<NA>(A, r + 1 + k, raw[k], fast_cols, sy0, sy1, sye, N);
-            emit_row<NA, REDUCE>(A, r + k, y0, st2, st1, P, C, N, acc);
+            if (r + 1 + k + U <= rB) load_row<NA, NT>(A, r + 1 + k + U, y0, ye, edge_ok, raw[k]);
+            emit_row<NA, REDUCE, NT>(A, r + k, y0, st2, st1, P, C, N, acc);
             copy_row<NA>(P, C);
             copy_row<NA>(C, N);
         }
@@ -402,28 +417,48 @@ constexpr int prefetch_rows() {
     return NA == 1 ? 8 : (NA == 2 ? 4 : 2);
 }
 
-template <int NA>
-hipError_t launch_pass_na(bool reduce, const PassArgs& a, hipStream_t s) {
+template <int NA, int U, int NT>
+hipError_t launch_v(bool reduce, const PassArgs& a, hipStream_t s) {
     const long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
-    constexpr int U = prefetch_rows<NA>();
     if (reduce)
-        hipLaunchKernelGGL((mm_pass_kernel<NA, U, true>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                           s, a);
+        hipLaunchKernelGGL((mm_pass_kernel<NA, U, true, NT>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((mm_pass_kernel<NA, U, false>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                           s, a);
+        hipLaunchKernelGGL((mm_pass_kernel<NA, U, false, NT>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, s, a);
     return hipGetLastError();
+}
+
+template <int NA>
+hipError_t launch_pass_na(bool reduce, const PassArgs& a, hipStream_t s, int variant) {
+    (void)variant;
+    return launch_v<NA, prefetch_rows<NA>(), 0>(reduce, a, s);
+}
+
+// one attribute: tuning variants (prefetch rows x non-temporal policy), see
+// tools/sweep.py; variant 0 is the default
+template <>
+hipError_t launch_pass_na<1>(bool reduce, const PassArgs& a, hipStream_t s, int variant) {
+    switch (variant) {
+        case 1: return launch_v<1, 4, 0>(reduce, a, s);
+        case 2: return launch_v<1, 16, 0>(reduce, a, s);
+        case 3: return launch_v<1, 8, 1>(reduce, a, s);
+        case 4: return launch_v<1, 8, 3>(reduce, a, s);
+        case 5: return launch_v<1, 4, 1>(reduce, a, s);
+        case 6: return launch_v<1, 16, 1>(reduce, a, s);
+        default: return launch_v<1, 8, 0>(reduce, a, s);
+    }
 }
 
 }  // namespace
 
-hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s) {
+hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant) {
     if (a.waves_total <= 0) return hipSuccess;
     switch (na) {
-        case 1: return launch_pass_na<1>(reduce, a, s);
-        case 2: return launch_pass_na<2>(reduce, a, s);
-        case 3: return launch_pass_na<3>(reduce, a, s);
-        case 4: return launch_pass_na<4>(reduce, a, s);
+        case 1: return launch_pass_na<1>(reduce, a, s, variant);
+        case 2: return launch_pass_na<2>(reduce, a, s, variant);
+        case 3: return launch_pass_na<3>(reduce, a, s, variant);
+        case 4: return launch_pass_na<4>(reduce, a, s, variant);
         default: return hipErrorInvalidValue;
     }
 }
