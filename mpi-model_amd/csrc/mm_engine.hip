@@ -335,16 +335,16 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_
     return MM_OK;
 }
 
+// Rows per wave of the step kernel (a compile-time row block: 8, 16 or 32). Short
+// blocks give the most waves in flight, which is what the memory system wants
+// (tools/sweep.py, profiles/r01): 8 by default, MM_ROWS_PER_WAVE overrides.
 int choose_th(const mm_engine* e) {
+    (void)e;
     if (const char* s = std::getenv("MM_ROWS_PER_WAVE")) {
-        int v = std::atoi(s);
-        if (v >= 1) return v;
+        const int v = std::atoi(s);
+        if (v == 8 || v == 16 || v == 32) return v;
     }
-    // aim for ~4096 waves (16 per CU on 256 CUs), rows per wave in [16, 512]
-    const long long target = 4096;
-    long long th = (e->d.h * (long long)e->nstrips + target - 1) / target;
-    th = std::max<long long>(16, std::min<long long>(512, th));
-    return (int)th;
+    return 8;
 }
 
 int ensure_partials(mm_engine* e) {
@@ -584,7 +584,15 @@ int mm_add_flow(mm_engine* e, int kind, int a, int b, double rate) {
     MM_HIP(hipStreamSynchronize(e->s_comp));
     e->flows.push_back({kind, a, kind == MM_FLOW_TRANSFER ? (b < 0 ? -1 : b) : a, rate});
     drop_graphs(e);
-    return compile_passes(e);
+    MM_TRY(compile_passes(e));
+    // transfers or several attributes: the generic kernel exists for 8-row blocks only
+    bool chains = e->na > 1;
+    for (const Pass& p : e->passes) chains = chains || !p.pre.empty() || !p.post.empty();
+    if (chains && e->th != 8) {
+        e->th = 8;
+        MM_TRY(ensure_partials(e));
+    }
+    return MM_OK;
 }
 
 int mm_point_apply(mm_engine* e, int attr, long long sx, long long sy, double captured,

@@ -47,10 +47,16 @@ __device__ __forceinline__ double share_of(double out, int cnt) {
     return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
 }
 
+// Chain entries are read with compile-time indices only, so they are scalar loads of
+// the kernel arguments that the compiler hoists out of the row loop (a runtime index
+// into the by-value PassArgs turns into per-row global loads and vmcnt(0) waits that
+// drain the row prefetch).
 template <int NA>
 __device__ __forceinline__ void apply_chain(double (&u)[NA], int n, const signed char* ta,
                                             const signed char* tb, const double* tr) {
-    for (int t = 0; t < n; ++t) {
+#pragma unroll
+    for (int t = 0; t < kMaxChain; ++t) {
+        if (t >= n) break;  // wave-uniform
         const int a = ta[t], b = tb[t];
         const double r = tr[t];
         double src = 0.0;
@@ -81,26 +87,39 @@ struct ProcRow {
 };
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr unsigned kOOB = 0x80000000u;  // voffset past any num_records: loads 0, stores dropped
+
+// Buffer descriptor of local row r of one attribute buffer. Rows outside [0, rmax] get
+// num_records = 0: their loads return 0 and their stores are dropped with no memory
+// traffic, so every loop iteration issues the same memory instructions (the compiler
+// can then keep counted vmcnt waits across the loop instead of draining it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* buf, int r, int rmax,
+                                                           long long pitch) {
+    const bool ok = r <= rmax;
+    const double* p = buf + (long long)(ok ? r : 0) * pitch;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0,
+                                             ok ? (int)(pitch * 8) : 0, 0x00020000);
+}
 
 // NT bit 1: non-temporal loads; bit 0: non-temporal stores
 template <int NA, int NT>
-__device__ __forceinline__ void load_row(const PassArgs& A, int r, long long y0, long long ye,
-                                         bool edge_ok, RawRow<NA>& o) {
+__device__ __forceinline__ void load_row(const PassArgs& A, int r, int rmax, unsigned voff,
+                                         unsigned eoff, RawRow<NA>& o) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        const double* row = A.in[a] + (long long)r * A.pitch;
-        dv2 p;
-        if (NT & 2)
-            p = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(row + y0));
-        else
-            p = *reinterpret_cast<const dv2*>(row + y0);
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc(A.in[a], r, rmax, A.pitch);
+        const dv2 p = __builtin_bit_cast(
+            dv2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, (NT & 2) ? 2 : 0));
         o.v0[a] = p.x;
         o.v1[a] = p.y;
-        o.ve[a] = edge_ok ? row[ye] : 0.0;
+        o.ve[a] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, eoff, 0, 0));
     }
 }
 
-template <int NA>
+template <int NA, bool CHAIN>
 __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawRow<NA>& raw,
                                             bool fast_cols, int sy0, int sy1, int sye,
                                             ProcRow<NA>& o) {
@@ -113,7 +132,7 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
         u1[a] = raw.v1[a];
         ue[a] = raw.ve[a];
     }
-    if (A.npre) {
+    if (CHAIN && A.npre) {
         apply_chain<NA>(u0, A.npre, A.pre_a, A.pre_b, A.pre_r);
         apply_chain<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
         apply_chain<NA>(ue, A.npre, A.pre_a, A.pre_b, A.pre_r);
@@ -169,10 +188,11 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
     }
 }
 
-template <int NA, bool REDUCE, int NT>
-__device__ __forceinline__ void emit_row(const PassArgs& A, int r, long long y0, bool st2,
-                                         bool st1, const ProcRow<NA>& P, const ProcRow<NA>& C,
-                                         const ProcRow<NA>& N, double (&acc)[NA]) {
+template <int NA, bool REDUCE, int NT, bool CHAIN>
+__device__ __forceinline__ void emit_row(const PassArgs& A, int r, int rmax, unsigned voff,
+                                         bool st2, bool st1, const ProcRow<NA>& P,
+                                         const ProcRow<NA>& C, const ProcRow<NA>& N,
+                                         double (&acc)[NA]) {
     double w0[NA], w1[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -192,27 +212,23 @@ __device__ __forceinline__ void emit_row(const PassArgs& A, int r, long long y0,
             w1[a] = C.d1[a];
         }
     }
-    if (A.npost) {
+    if (CHAIN && A.npost) {
         apply_chain<NA>(w0, A.npost, A.post_a, A.post_b, A.post_r);
         apply_chain<NA>(w1, A.npost, A.post_a, A.post_b, A.post_r);
     }
+    const bool live = r <= rmax;  // wave-uniform
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        double* row = A.out[a] + (long long)r * A.pitch;
-        if (st2) {
-            dv2 v;
-            v.x = w0[a];
-            v.y = w1[a];
-            if (NT & 1)
-                __builtin_nontemporal_store(v, reinterpret_cast<dv2*>(row + y0));
-            else
-                *reinterpret_cast<dv2*>(row + y0) = v;
-        } else if (st1) {
-            row[y0] = w0[a];
-        }
+        dv2 v;
+        v.x = w0[a];
+        v.y = w1[a];
+        // lanes past W write the row's padding columns (never read as cells)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v),
+                                               row_rsrc(A.out[a], r, rmax, A.pitch), voff, 0,
+                                               (NT & 1) ? 2 : 0);
         if (REDUCE) {
-            if (st1) acc[a] = acc[a] + w0[a];
-            if (st2) acc[a] = acc[a] + w1[a];
+            acc[a] = acc[a] + ((live && st1) ? w0[a] : 0.0);
+            acc[a] = acc[a] + ((live && st2) ? w1[a] : 0.0);
         }
     }
 }
@@ -236,11 +252,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-template <int NA, int U, bool REDUCE, int NT>
+// TH output rows per wave, fully unrolled (no loop back edge, so the compiler keeps
+// counted vmcnt waits for every row instead of draining at a loop header).
+template <int NA, int TH, int U, bool REDUCE, int NT, bool CHAIN>
 __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
+    static_assert(U <= TH, "prefetch deeper than the row block");
     const int lane = threadIdx.x & 63;
-    const long long wid =
-        (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);  // wave-uniform
+    // wave-uniform, and provably so for the compiler (scalar descriptors, no waterfalls)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long wid = (long long)blockIdx.x * kWavesPerBlock + wave;
     if (wid >= A.waves_total) return;
 
     // wave -> (row range, row block, column strip); strips vary fastest so the 4 waves of
@@ -257,8 +277,8 @@ __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
     }
     const int strip = (int)(w % A.nstrips);
     const int rb = (int)(w / A.nstrips);
-    const int rA = rlo + rb * A.th;
-    const int rB = min(rA + A.th, rhi);
+    const int rA = rlo + rb * TH;
+    const int rB = min(rA + TH, rhi);  // output rows [rA, rB); input rows [rA-1, rB]
 
     const long long base = (long long)strip * kStripCols;
     const long long y0 = base + 2 * lane;
@@ -269,33 +289,33 @@ __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
     const int sy0 = span3(W, y0), sy1 = span3(W, y0 + 1), sye = edge_ok ? span3(W, ye) : 0;
     const bool fast_cols = base >= 2 && base + kStripCols <= W - 2;  // wave-uniform
     const bool st1 = y0 < W, st2 = y0 + 1 < W;
+    const unsigned voff = (unsigned)(y0 * 8);
+    const unsigned eoff = edge_ok ? (unsigned)(ye * 8) : kOOB;
 
     double acc[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) acc[a] = 0.0;
 
-    // Rolling prefetch: raw[k] holds input row r+1+k of the current group of U output
-    // rows; right after row r+k is emitted, raw[k] is refilled with row r+1+k+U, so U
-    // row loads stay in flight for the whole strip.
+    // Input row rA-1+i is "input i". Inputs 0 and 1 prime the window; input i >= 2
+    // lives in raw[(i-2) % U] and is refilled with input i+U as soon as it is consumed,
+    // so U row loads stay in flight down the strip. Rows past rB load as zeros without
+    // traffic and output rows past rB-1 are dropped (descriptors with num_records 0).
     RawRow<NA> first, second, raw[U];
-    load_row<NA, NT>(A, rA - 1, y0, ye, edge_ok, first);
-    load_row<NA, NT>(A, rA, y0, ye, edge_ok, second);
+    load_row<NA, NT>(A, rA - 1, rB, voff, eoff, first);
+    load_row<NA, NT>(A, rA, rB, voff, eoff, second);
 #pragma unroll
-    for (int k = 0; k < U; ++k)
-        if (rA + 1 + k <= rB) load_row<NA, NT>(A, rA + 1 + k, y0, ye, edge_ok, raw[k]);
+    for (int k = 0; k < U; ++k) load_row<NA, NT>(A, rA + 1 + k, rB, voff, eoff, raw[k]);
     ProcRow<NA> P, C, N;
-    process_row<NA>(A, rA - 1, first, fast_cols, sy0, sy1, sye, P);
-    process_row<NA>(A, rA, second, fast_cols, sy0, sy1, sye, C);
-    for (int r = rA; r < rB; r += U) {
+    process_row<NA, CHAIN>(A, rA - 1, first, fast_cols, sy0, sy1, sye, P);
+    process_row<NA, CHAIN>(A, rA, second, fast_cols, sy0, sy1, sye, C);
 #pragma unroll
-        for (int k = 0; k < U; ++k) {
-            if (r + k >= rB) break;  // wave-uniform
-            process_row<NA>(A, r + 1 + k, raw[k], fast_cols, sy0, sy1, sye, N);
-            if (r + 1 + k + U <= rB) load_row<NA, NT>(A, r + 1 + k + U, y0, ye, edge_ok, raw[k]);
-            emit_row<NA, REDUCE, NT>(A, r + k, y0, st2, st1, P, C, N, acc);
-            copy_row<NA>(P, C);
-            copy_row<NA>(C, N);
-        }
+    for (int k = 0; k < TH; ++k) {
+        process_row<NA, CHAIN>(A, rA + 1 + k, raw[k % U], fast_cols, sy0, sy1, sye, N);
+        if (k + U < TH)  // input k+2+U is still inside this row block
+            load_row<NA, NT>(A, rA + 1 + k + U, rB, voff, eoff, raw[k % U]);
+        emit_row<NA, REDUCE, NT, CHAIN>(A, rA + k, rB - 1, voff, st2, st1, P, C, N, acc);
+        copy_row<NA>(P, C);
+        copy_row<NA>(C, N);
     }
 
     if (REDUCE) {
@@ -410,43 +430,57 @@ __global__ void mm_sum_partials_kernel(const double* partials, long long n, doub
     if (threadIdx.x == 0) *out = red[0];
 }
 
-// rows kept in flight per wave: 8 KiB per wave at one attribute, fewer rows as the
-// attributes (and the registers per row) grow
+template <int NA, int TH, int U, int NT, bool CHAIN>
+hipError_t launch_c(bool reduce, const PassArgs& a, hipStream_t s) {
+    const long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (reduce)
+        hipLaunchKernelGGL((mm_pass_kernel<NA, TH, U, true, NT, CHAIN>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((mm_pass_kernel<NA, TH, U, false, NT, CHAIN>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+// One attribute, no transfers: the headline Exponencial step. Row block TH in
+// {8, 16, 32} (a.th), non-temporal policy from the tuning variant (0 none, 1 stores,
+// 3 loads+stores).
+template <int TH>
+hipError_t launch_one(bool reduce, const PassArgs& a, hipStream_t s, int variant) {
+    switch (variant) {
+        case 1: return launch_c<1, TH, 8, 1, false>(reduce, a, s);
+        case 3: return launch_c<1, TH, 8, 3, false>(reduce, a, s);
+        default: return launch_c<1, TH, 8, 0, false>(reduce, a, s);
+    }
+}
+
+// rows kept in flight per wave: 8 KiB at one attribute, fewer rows as the attributes
+// (and the registers per row) grow
 template <int NA>
 constexpr int prefetch_rows() {
     return NA == 1 ? 8 : (NA == 2 ? 4 : 2);
 }
 
-template <int NA, int U, int NT>
-hipError_t launch_v(bool reduce, const PassArgs& a, hipStream_t s) {
-    const long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (reduce)
-        hipLaunchKernelGGL((mm_pass_kernel<NA, U, true, NT>), dim3((unsigned)blocks),
-                           dim3(kBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL((mm_pass_kernel<NA, U, false, NT>), dim3((unsigned)blocks),
-                           dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
 template <int NA>
 hipError_t launch_pass_na(bool reduce, const PassArgs& a, hipStream_t s, int variant) {
     (void)variant;
-    return launch_v<NA, prefetch_rows<NA>(), 0>(reduce, a, s);
+    constexpr int U = prefetch_rows<NA>();
+    if (a.th != 8) return hipErrorInvalidValue;
+    if (a.npre || a.npost) return launch_c<NA, 8, U, 0, true>(reduce, a, s);
+    return launch_c<NA, 8, U, 0, false>(reduce, a, s);
 }
 
-// one attribute: tuning variants (prefetch rows x non-temporal policy), see
-// tools/sweep.py; variant 0 is the default
 template <>
 hipError_t launch_pass_na<1>(bool reduce, const PassArgs& a, hipStream_t s, int variant) {
-    switch (variant) {
-        case 1: return launch_v<1, 4, 0>(reduce, a, s);
-        case 2: return launch_v<1, 16, 0>(reduce, a, s);
-        case 3: return launch_v<1, 8, 1>(reduce, a, s);
-        case 4: return launch_v<1, 8, 3>(reduce, a, s);
-        case 5: return launch_v<1, 4, 1>(reduce, a, s);
-        case 6: return launch_v<1, 16, 1>(reduce, a, s);
-        default: return launch_v<1, 8, 0>(reduce, a, s);
+    if (a.npre || a.npost) {
+        if (a.th != 8) return hipErrorInvalidValue;
+        return launch_c<1, 8, 8, 0, true>(reduce, a, s);
+    }
+    switch (a.th) {
+        case 8: return launch_one<8>(reduce, a, s, variant);
+        case 16: return launch_one<16>(reduce, a, s, variant);
+        case 32: return launch_one<32>(reduce, a, s, variant);
+        default: return hipErrorInvalidValue;
     }
 }
 

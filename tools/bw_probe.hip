@@ -48,19 +48,22 @@ __global__ __launch_bounds__(256) void walk(const double* in, double* out, long 
     const long long strip = wid % nstrips, rb = wid / nstrips;
     const long long r0 = rb * TH;
     if (r0 >= H) return;
+    const int rows = (int)(r0 + TH <= H ? TH : H - r0);  // rows of this wave, never past H
     auto off = [&](long long r) {
         return STRIP_MAJOR ? (strip * H + r) * 128 + 2 * lane : r * W + strip * 128 + 2 * lane;
     };
     dv2 buf[U];
 #pragma unroll
     for (int k = 0; k < U; ++k)
-        buf[k] = NT ? __builtin_nontemporal_load((const dv2*)(in + off(r0 + k)))
-                    : *(const dv2*)(in + off(r0 + k));
-    for (int r = 0; r < TH; r += U) {
+        if (k < rows)
+            buf[k] = NT ? __builtin_nontemporal_load((const dv2*)(in + off(r0 + k)))
+                        : *(const dv2*)(in + off(r0 + k));
+    for (int r = 0; r < rows; r += U) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
+            if (r + k >= rows) break;
             dv2 v = buf[k];
-            if (r + k + U < TH)
+            if (r + k + U < rows)
                 buf[k] = NT ? __builtin_nontemporal_load((const dv2*)(in + off(r0 + r + k + U)))
                             : *(const dv2*)(in + off(r0 + r + k + U));
             v = v * 0.5;

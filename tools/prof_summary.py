@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of scripts/gpu_profile.sh for the step kernel.
+
+Kernel time: the kernel-trace stats CSV (average duration per kernel name).
+HBM traffic per launch: FETCH_SIZE and WRITE_SIZE (KB) per dispatch of mm_pass_kernel,
+averaged; FETCH_SIZE doubled, the gfx950 correction of MI355X_MICROARCH.md 'HBM'
+(it counts 64 B per 128-B request of a wide coalesced stream).
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KERNEL = "mm_pass_kernel"
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def main():
+    d, wl = sys.argv[1], sys.argv[2]
+    res = {"workload": wl}
+    stats = rows(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
+    for r in stats:
+        if KERNEL in r.get("Name", ""):
+            res["kernel_name"] = r["Name"][:120]
+            res["calls"] = int(r["Calls"])
+            res["avg_us"] = float(r["AverageNs"]) / 1e3
+            res["min_us"] = float(r["MinNs"]) / 1e3
+            res["max_us"] = float(r["MaxNs"]) / 1e3
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
+                if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter]
+        if vals:
+            res[counter + "_KB_avg"] = statistics.mean(vals)
+            res[counter + "_dispatches"] = len(vals)
+    if "FETCH_SIZE_KB_avg" in res and "WRITE_SIZE_KB_avg" in res:
+        rd = 2.0 * res["FETCH_SIZE_KB_avg"] * 1024
+        wr = res["WRITE_SIZE_KB_avg"] * 1024
+        res["hbm_read_bytes_per_launch"] = rd
+        res["hbm_write_bytes_per_launch"] = wr
+        res["hbm_bytes_per_launch"] = rd + wr
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -36,8 +36,8 @@ def time_engine(e, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
-    ap.add_argument("--ths", default="8,16,32,64,128")
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6")
+    ap.add_argument("--ths", default="8,16,32")
+    ap.add_argument("--variants", default="0,1,3")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
