@@ -86,7 +86,7 @@ typedef struct mm_info {
     long long waves_per_pass;  /* waves launched per pass */
     long long steps_done;      /* steps run since the last fill/upload */
     int fused_attrs;           /* attributes carried per fused pass */
-    int reserved;
+    int steps_per_launch;      /* 2: the program runs as fused step pairs (temporal blocking) */
 } mm_info;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -117,8 +117,10 @@ int mm_device_count(int* n);
 
 /* ---- engine ------------------------------------------------------------- */
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
- * init loop (src/Model.hpp:154-157): device buffers are (h+2) x pitch fp64 per
- * attribute (one ghost row above and below), two of them (Jacobi ping-pong). */
+ * init loop (src/Model.hpp:154-157): device buffers are (h+4) x pitch fp64 per
+ * attribute (two ghost rows above and below), two of them (Jacobi ping-pong).
+ * Environment: MM_FUSE=0 disables the fused two-step kernel, MM_ROWS_PER_WAVE
+ * (8/16/32) and MM_KERNEL_VARIANT (non-temporal policy) override tuning. */
 int mm_engine_create(const mm_desc* desc, mm_engine** out);
 int mm_engine_destroy(mm_engine* eng);
 int mm_engine_info(mm_engine* eng, mm_info* info);
@@ -166,8 +168,9 @@ int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
 
 /* Measurement: with timing on, mm_run records a HIP event pair around every
  * step-kernel launch on the stream it is launched on; mm_timing returns the
- * number of timed launches, their summed duration (ms) and the algorithmic
- * bytes one launch moves (16 B per cell per attribute). */
+ * number of timed launches, their summed duration (ms) and the average algorithmic
+ * bytes one launch moves: 16 B per cell of its rows per attribute (read once, written
+ * once), for a one-step launch and a fused two-step launch alike. */
 int mm_set_timing(mm_engine* eng, int on);
 int mm_timing(mm_engine* eng, long long* n_launches, double* total_ms, double* bytes_per_launch);
 

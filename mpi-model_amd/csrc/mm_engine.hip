@@ -1,8 +1,10 @@
 // mm_engine.hip -- the host engine behind include/mpimodel.h (C ABI).
 //
 // One engine = one row slab of the global grid on one GPU:
-//   * device memory: per attribute two (h+2) x pitch fp64 buffers (Jacobi
-//     ping-pong), local row 0 / h+1 are ghost rows, pitch a multiple of 128;
+//   * device memory: per attribute two (h+4) x pitch fp64 buffers (Jacobi
+//     ping-pong) with two ghost rows above and below, pitch a multiple of 128;
+//   * a single-attribute, single-diffusion program runs two steps per kernel pass
+//     (mm_pass2_kernel, temporal blocking: half the HBM traffic per cell-update);
 //   * a compute stream and a comm stream; with MM_HALO_RCCL each pass first
 //     exchanges border rows with ncclSend/ncclRecv on the comm stream while the
 //     interior rows run on the compute stream, then the two border rows run;
@@ -78,7 +80,7 @@ struct mm_engine {
     mm_desc d{};
     int na = 1;
     long long pitch = 0;
-    long long rows_alloc = 0;  // h + 2
+    long long rows_alloc = 0;  // h + 2 * kGhost
     double* base = nullptr;
     size_t bytes = 0;
     double* buf[2][mm::kMaxAttr] = {};
@@ -107,11 +109,15 @@ struct mm_engine {
     // graph cache: key = (parity, length, reduce_every)
     std::map<std::tuple<int, long long, long long>, hipGraphExec_t> graphs;
 
+    bool fuse_ok = true;  // MM_FUSE=0 disables the two-step kernel
+
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
+    std::vector<double> ev_bytes;  // algorithmic bytes of each timed launch (pairs of events)
     size_t ev_used = 0;
     long long timed_launches = 0;
     double timed_ms = 0.0;
+    double timed_bytes = 0.0;
 };
 
 namespace {
@@ -205,94 +211,154 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
-int launch_timed(mm_engine* e, int na, bool reduce, const mm::PassArgs& A, bool time_it) {
+// Launch a pass (fused == 0) or a fused two-step pass (fused == 1, `red` = its RED mode)
+// covering `rows` rows, with an event pair around it when timing.
+int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long long rows,
+                 bool time_it) {
     hipEvent_t a = nullptr, b = nullptr;
     if (time_it) {
         a = next_event(e);
         b = next_event(e);
         if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
+        e->ev_bytes.resize(e->ev_used / 2);
+        e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * (fused ? 1 : e->na);
         MM_HIP(hipEventRecord(a, e->s_comp));
     }
-    MM_HIP(mm::launch_pass(na, reduce, A, e->s_comp, e->variant));
+    if (fused)
+        MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
+    else
+        MM_HIP(mm::launch_pass(e->na, red != 0, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
     return MM_OK;
 }
 
-int halo_rccl(mm_engine* e) {
+// Border-row exchange with both neighbours in one RCCL group: the first / last `depth`
+// owned rows go to rank-1 / rank+1, their rows land in the ghost rows. Rows are
+// contiguous (pitch doubles each), so every message is one contiguous block.
+int halo_rccl(mm_engine* e, int depth) {
     const int r = e->d.rank, n = e->d.nranks;
-    const long long W = e->d.W, P = e->pitch, h = e->d.h;
+    const long long P = e->pitch, h = e->d.h;
+    const size_t cnt = (size_t)(depth * P);
     MM_NCCL(ncclGroupStart());
     for (int a = 0; a < e->na; ++a) {
         double* b = e->buf[e->cur][a];
         if (r > 0) {
-            MM_NCCL(ncclSend(b + 1 * P, (size_t)W, ncclDouble, r - 1, e->comm, e->s_comm));
-            MM_NCCL(ncclRecv(b + 0 * P, (size_t)W, ncclDouble, r - 1, e->comm, e->s_comm));
+            MM_NCCL(ncclSend(b, cnt, ncclDouble, r - 1, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b - depth * P, cnt, ncclDouble, r - 1, e->comm, e->s_comm));
         }
         if (r < n - 1) {
-            MM_NCCL(ncclSend(b + h * P, (size_t)W, ncclDouble, r + 1, e->comm, e->s_comm));
-            MM_NCCL(ncclRecv(b + (h + 1) * P, (size_t)W, ncclDouble, r + 1, e->comm, e->s_comm));
+            MM_NCCL(ncclSend(b + (h - depth) * P, cnt, ncclDouble, r + 1, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b + h * P, cnt, ncclDouble, r + 1, e->comm, e->s_comm));
         }
     }
     MM_NCCL(ncclGroupEnd());
     return MM_OK;
 }
 
-// Enqueue one step (all passes). reduce: append the per-attribute sums to the history.
-int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
+int begin_halo(mm_engine* e, int depth) {
+    MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
+    MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
+    MM_TRY(halo_rccl(e, depth));
+    MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
+    return MM_OK;
+}
+
+// Rows [lo, hi) of the slab as range a, optional [lo2, hi2) as range b.
+void set_ranges(const mm_engine* e, mm::PassArgs& A, long long lo, long long hi, long long lo2,
+                long long hi2) {
+    A.ra0 = (int)lo;
+    A.ra1 = (int)hi;
+    A.rb0 = (int)lo2;
+    A.rb1 = (int)hi2;
+    A.waves_a = waves_for(e, hi - lo);
+    A.waves_total = A.waves_a + waves_for(e, hi2 - lo2);
+}
+
+// One kernel pass over the slab, with the halo of `depth` rows exchanged first. With the
+// RCCL halo the interior rows (which need no ghost row) run while the rows are in flight,
+// then the `depth` border rows on each side. `entries` history entries of n_attr sums
+// are appended when red != 0 (fused: red 1 -> 1 entry, red 2 -> 2 entries).
+int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it) {
     const long long h = e->d.h;
-    const int np = (int)e->passes.size();
-    for (int pi = 0; pi < np; ++pi) {
-        const Pass& p = e->passes[pi];
-        const bool red = reduce && pi == np - 1;
-        mm::PassArgs A;
-        fill_args(e, p, A);
-        if (e->split && h >= 3) {
-            MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
-            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
-            MM_TRY(halo_rccl(e));
-            MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
-            // interior rows 2..h-1 need no ghost row
-            A.ra0 = 2;
-            A.ra1 = (int)h;
-            A.rb0 = A.rb1 = 0;
-            A.waves_a = waves_for(e, h - 2);
-            A.waves_total = A.waves_a;
-            A.partial_base = 0;
-            MM_TRY(launch_timed(e, e->na, red, A, time_it));
+    const int depth = fused ? 2 : 1;
+    const int entries = (fused && red == 2) ? 2 : 1;
+    const int per_wave = fused ? entries : e->na;
+    mm::PassArgs A;
+    fill_args(e, p, A);
+    long long total_waves = 0;
+    if (e->split && h >= 2 * depth + 1) {
+        MM_TRY(begin_halo(e, depth));
+        set_ranges(e, A, depth, h - depth, 0, 0);
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, fused, red, A, h - 2 * depth, time_it));
+        total_waves = A.waves_total;
+        MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
+        set_ranges(e, A, 0, depth, h - depth, h);
+        A.partial_base = total_waves;
+        if (fused)
+            MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
+        else
+            MM_HIP(mm::launch_pass(e->na, red != 0, A, e->s_comp, e->variant));
+        total_waves += A.waves_total;
+    } else {
+        if (e->split) {  // slab too thin to split: exchange first, then one launch
+            MM_TRY(begin_halo(e, depth));
             MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
-            // border rows 1 and h
-            const long long wa = A.waves_total;
-            A.ra0 = 1;
-            A.ra1 = 2;
-            A.rb0 = (int)h;
-            A.rb1 = (int)h + 1;
-            A.waves_a = waves_for(e, 1);
-            A.waves_total = 2 * A.waves_a;
-            A.partial_base = wa;
-            MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
-            if (red)
-                MM_HIP(mm::launch_finalize(e->partials, wa + A.waves_total, e->na, e->hist,
-                                           e->hist_n, e->hist_cap, e->s_comp));
-        } else {
-            if (e->split) {  // tiny slab (h < 3): exchange first, then one launch
-                MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
-                MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
-                MM_TRY(halo_rccl(e));
-                MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
-                MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
-            }
-            A.ra0 = 1;
-            A.ra1 = (int)h + 1;
-            A.rb0 = A.rb1 = 0;
-            A.waves_a = waves_for(e, h);
-            A.waves_total = A.waves_a;
-            A.partial_base = 0;
-            MM_TRY(launch_timed(e, e->na, red, A, time_it));
-            if (red)
-                MM_HIP(mm::launch_finalize(e->partials, A.waves_total, e->na, e->hist, e->hist_n,
-                                           e->hist_cap, e->s_comp));
         }
-        e->cur ^= 1;
+        set_ranges(e, A, 0, h, 0, 0);
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, fused, red, A, h, time_it));
+        total_waves = A.waves_total;
+    }
+    if (red)
+        MM_HIP(mm::launch_finalize(e->partials, total_waves, fused ? 1 : e->na, e->hist,
+                                   e->hist_n, e->hist_cap, e->s_comp, fused ? entries : 1));
+    (void)per_wave;
+    e->cur ^= 1;
+    return MM_OK;
+}
+
+// One step (all passes); reduce: append the per-attribute sums to the history.
+int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
+    const int np = (int)e->passes.size();
+    for (int pi = 0; pi < np; ++pi)
+        MM_TRY(enqueue_pass(e, e->passes[pi], false, (reduce && pi == np - 1) ? 1 : 0, time_it));
+    return MM_OK;
+}
+
+// Two steps in one fused pass; r1 / r2: reduce after the first / second step.
+int enqueue_pair(mm_engine* e, bool r1, bool r2, bool time_it) {
+    if (r1 && !r2) {  // no kernel mode for "first step only": run the steps singly
+        MM_TRY(enqueue_step(e, true, time_it));
+        return enqueue_step(e, false, time_it);
+    }
+    return enqueue_pass(e, e->passes[0], true, r1 ? 2 : (r2 ? 1 : 0), time_it);
+}
+
+// Can steps run as fused pairs? One attribute, one pass that is a single diffusion.
+bool fusable(const mm_engine* e) {
+    if (!e->fuse_ok || e->na != 1 || e->passes.size() != 1) return false;
+    const Pass& p = e->passes[0];
+    if (!p.pre.empty() || !p.post.empty() || p.diffuse_mask != 1) return false;
+    if (e->d.nranks > 1 && e->d.halo_mode != MM_HALO_RCCL) return false;
+    return e->th == 8 || e->th == 16;
+}
+
+// Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
+int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_every,
+                  bool time_it) {
+    const bool fuse = fusable(e);
+    long long s = first;
+    const long long end = first + n;
+    auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
+    while (s < end) {
+        if (fuse && s + 1 < end) {
+            MM_TRY(enqueue_pair(e, red(s), red(s + 1), time_it));
+            s += 2;
+        } else {
+            MM_TRY(enqueue_step(e, red(s), time_it));
+            s += 1;
+        }
     }
     return MM_OK;
 }
@@ -315,9 +381,7 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_
     }
     const int cur0 = e->cur;
     MM_HIP(hipStreamBeginCapture(e->s_comp, hipStreamCaptureModeThreadLocal));
-    int rc = MM_OK;
-    for (long long i = 1; i <= len && rc == MM_OK; ++i)
-        rc = enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false);
+    const int rc = enqueue_steps(e, 1, len, reduce_every, false);
     hipGraph_t g = nullptr;
     hipError_t ec = hipStreamEndCapture(e->s_comp, &g);
     e->cur = cur0;  // capture only recorded the work; the state advances at replay
@@ -444,8 +508,12 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->na = d.n_attr;
     e->pitch = (d.W + mm::kStripCols - 1) / mm::kStripCols * mm::kStripCols;
     e->nstrips = (int)(e->pitch / mm::kStripCols);
-    e->rows_alloc = d.h + 2;
+    e->rows_alloc = d.h + 2 * mm::kGhost;
+    if (const char* f = std::getenv("MM_FUSE")) e->fuse_ok = std::atoi(f) != 0;
     e->th = choose_th(e);
+    // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
+    // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
+    e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
     if (const char* v = std::getenv("MM_KERNEL_VARIANT")) e->variant = std::atoi(v);
 
     auto cleanup = [&](int rc) {
@@ -463,7 +531,8 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     he = hipMemset(e->base, 0, e->bytes);
     if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(he)));
     for (int k = 0; k < 2; ++k)
-        for (int a = 0; a < e->na; ++a) e->buf[k][a] = e->base + per_al * (size_t)(k * e->na + a);
+        for (int a = 0; a < e->na; ++a)
+            e->buf[k][a] = e->base + per_al * (size_t)(k * e->na + a) + mm::kGhost * e->pitch;
 
     if (hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking) != hipSuccess ||
@@ -526,6 +595,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->waves_per_pass = waves_for(e, e->d.h);
     info->steps_done = e->steps_done;
     info->fused_attrs = e->na;
+    info->steps_per_launch = fusable(e) ? 2 : 1;
     return MM_OK;
 }
 
@@ -543,7 +613,7 @@ int mm_fill(mm_engine* e, int attr, int mode, double value, unsigned long long s
 int mm_upload(mm_engine* e, int attr, const double* host) {
     if (!e || !host || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_upload: bad arguments");
     MM_TRY(set_device(e));
-    MM_HIP(hipMemcpy2DAsync(e->buf[e->cur][attr] + e->pitch, sizeof(double) * e->pitch, host,
+    MM_HIP(hipMemcpy2DAsync(e->buf[e->cur][attr], sizeof(double) * e->pitch, host,
                             sizeof(double) * e->d.W, sizeof(double) * e->d.W, e->d.h,
                             hipMemcpyHostToDevice, e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comp));
@@ -555,7 +625,7 @@ int mm_download(mm_engine* e, int attr, double* host) {
     if (!e || !host || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_download: bad arguments");
     MM_TRY(set_device(e));
     MM_HIP(hipStreamSynchronize(e->s_comm));
-    MM_HIP(hipMemcpy2DAsync(host, sizeof(double) * e->d.W, e->buf[e->cur][attr] + e->pitch,
+    MM_HIP(hipMemcpy2DAsync(host, sizeof(double) * e->d.W, e->buf[e->cur][attr],
                             sizeof(double) * e->pitch, sizeof(double) * e->d.W, e->d.h,
                             hipMemcpyDeviceToHost, e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comp));
@@ -617,35 +687,29 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     MM_TRY(set_device(e));
     const int np = (int)e->passes.size();
     if (e->timing) {  // eager launches with an event pair around each step kernel
-        for (long long i = 1; i <= nsteps; ++i)
-            MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, true));
+        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, true));
         e->steps_done += nsteps;
         return MM_OK;
     }
-    // graph of one ping-pong cycle (and of the reduction period), replayed
-    const long long cycle = (np % 2) ? 2 : 1;
-    long long len = cycle;
-    if (reduce_every > 0) len = cycle / gcd_ll(cycle, reduce_every) * reduce_every;
+    // Replay a graph of `per` steps: a whole number of fused pairs, an even number of
+    // buffer flips (so the captured pointers are valid again) and of reduction periods.
+    const bool fuse = fusable(e);
+    const long long unit = fuse ? 2 : 1;
+    const long long flips = fuse ? 1 : np;
+    long long len = unit * ((flips % 2) ? 2 : 1);
+    if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
     if (len > 256 || nsteps < len) {
-        for (long long i = 1; i <= nsteps; ++i)
-            MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false));
+        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, false));
         e->steps_done += nsteps;
         return MM_OK;
     }
-    // replay graph chunks of `len` steps; at least a few steps per replay
     long long per = len;
-    while (per < 8 && per * 2 <= nsteps) per *= 2;
+    while (per < 16 && per * 2 <= nsteps) per *= 2;
     hipGraphExec_t g = nullptr;
     MM_TRY(get_graph(e, per, reduce_every, &g));
     long long done = 0;
-    for (; done + per <= nsteps; done += per) {
-        MM_HIP(hipGraphLaunch(g, e->s_comp));
-        if ((np * per) % 2) e->cur ^= 1;
-        // the graph was captured for a fixed parity: re-fetch if it flipped
-        if ((np * per) % 2) MM_TRY(get_graph(e, per, reduce_every, &g));
-    }
-    for (long long i = done + 1; i <= nsteps; ++i)
-        MM_TRY(enqueue_step(e, reduce_every > 0 && i % reduce_every == 0, false));
+    for (; done + per <= nsteps; done += per) MM_HIP(hipGraphLaunch(g, e->s_comp));
+    if (done < nsteps) MM_TRY(enqueue_steps(e, done + 1, nsteps - done, reduce_every, false));
     e->steps_done += nsteps;
     return MM_OK;
 }
@@ -697,10 +761,10 @@ int mm_halo_export(mm_engine* e, double* top, double* bottom) {
     const long long W = e->d.W, P = e->pitch, h = e->d.h;
     for (int a = 0; a < e->na; ++a) {
         if (top)
-            MM_HIP(hipMemcpyAsync(top + a * W, e->buf[e->cur][a] + 1 * P, sizeof(double) * W,
+            MM_HIP(hipMemcpyAsync(top + a * W, e->buf[e->cur][a], sizeof(double) * W,
                                   hipMemcpyDeviceToHost, e->s_comp));
         if (bottom)
-            MM_HIP(hipMemcpyAsync(bottom + a * W, e->buf[e->cur][a] + h * P, sizeof(double) * W,
+            MM_HIP(hipMemcpyAsync(bottom + a * W, e->buf[e->cur][a] + (h - 1) * P, sizeof(double) * W,
                                   hipMemcpyDeviceToHost, e->s_comp));
     }
     MM_HIP(hipStreamSynchronize(e->s_comp));
@@ -713,10 +777,10 @@ int mm_halo_import(mm_engine* e, const double* top, const double* bottom) {
     const long long W = e->d.W, P = e->pitch, h = e->d.h;
     for (int a = 0; a < e->na; ++a) {
         if (top)
-            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + 0 * P, top + a * W, sizeof(double) * W,
+            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] - P, top + a * W, sizeof(double) * W,
                                   hipMemcpyHostToDevice, e->s_comp));
         if (bottom)
-            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + (h + 1) * P, bottom + a * W,
+            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + h * P, bottom + a * W,
                                   sizeof(double) * W, hipMemcpyHostToDevice, e->s_comp));
     }
     MM_HIP(hipStreamSynchronize(e->s_comp));
@@ -729,8 +793,10 @@ int mm_set_timing(mm_engine* e, int on) {
     MM_HIP(hipStreamSynchronize(e->s_comp));
     e->timing = on != 0;
     e->ev_used = 0;
+    e->ev_bytes.clear();
     e->timed_launches = 0;
     e->timed_ms = 0.0;
+    e->timed_bytes = 0.0;
     return MM_OK;
 }
 
@@ -743,16 +809,16 @@ int mm_timing(mm_engine* e, long long* n, double* total_ms, double* bytes_per_la
         MM_HIP(hipEventElapsedTime(&ms, e->ev_pool[i], e->ev_pool[i + 1]));
         e->timed_ms += ms;
         e->timed_launches += 1;
+        e->timed_bytes += e->ev_bytes[i / 2];
     }
     e->ev_used = 0;
+    e->ev_bytes.clear();
     if (n) *n = e->timed_launches;
     if (total_ms) *total_ms = e->timed_ms;
-    if (bytes_per_launch) {
-        // algorithmic bytes of one full-slab launch: read + write 8 B per cell per attribute
-        int moved = 0;
-        if (!e->passes.empty()) moved = e->na;
-        *bytes_per_launch = 16.0 * (double)e->d.h * (double)e->d.W * moved;
-    }
+    // algorithmic bytes of a timed launch: each cell of its rows read once and written
+    // once per attribute (16 B), whether the launch advances one step or two
+    if (bytes_per_launch)
+        *bytes_per_launch = e->timed_launches ? e->timed_bytes / (double)e->timed_launches : 0.0;
     return MM_OK;
 }
 

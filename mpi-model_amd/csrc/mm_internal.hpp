@@ -11,9 +11,10 @@ constexpr int kMaxChain = 8;    // elementwise transfers before / after a pass's
 constexpr int kStripCols = 128; // columns per wave: 64 lanes x double2 (16 B per lane)
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
+constexpr int kGhost = 2;       // ghost rows above and below a slab (two fused steps need 2)
 
-// One fused Jacobi pass over a row slab (every buffer is (h+2) x pitch fp64,
-// local row 0 / h+1 are the ghost rows, local row r is global row x_init+r-1):
+// One fused Jacobi pass over a row slab. Every buffer pointer points at owned row 0;
+// rows -kGhost..-1 and h..h+kGhost-1 are ghost rows; local row r is global x_init+r.
 //   u  = pre-chain transfers applied to the loaded cell values
 //   per diffusing attribute a: out = rate_a*u, s = out/cnt, w = (u - out) + nb(s)
 //   w  = post-chain transfers applied to w;  store w
@@ -40,6 +41,9 @@ struct PassArgs {
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
 hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);
+// Two fused steps of a single-attribute, single-diffusion program (mm_pass2_kernel).
+// red: 0 no sums, 1 second step's sums (partials[wave]), 2 both (partials[wave][2]).
+hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant);
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
                        long long h, int mode, double value, unsigned long long seed, hipStream_t s);
 hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,
@@ -48,7 +52,8 @@ hipError_t launch_point(double* buf, long long pitch, long long H, long long W, 
 // Sum partials[n][na] in a fixed order into hist[k][na], k = (*hist_n)++ (device
 // counter, so the launch is graph-replayable); entries beyond cap are dropped.
 hipError_t launch_finalize(const double* partials, long long n, int na, double* hist,
-                           unsigned long long* hist_n, long long cap, hipStream_t s);
+                           unsigned long long* hist_n, long long cap, hipStream_t s,
+                           int entries = 1);
 // Per-attribute sum of the owned rows of one buffer (no pass), into out[0].
 hipError_t launch_slab_sum(const double* buf, long long pitch, long long W, long long h,
                            double* partials, long long nblocks, double* out_sum, hipStream_t s);

@@ -152,8 +152,60 @@ def test_timed_eager_path_equals_graph_path(gpu, O):
         a.run(20)
         b.run(20)
         n, ms, bytes_per = a.timing()
-        assert n == 20 and ms > 0 and bytes_per == 16.0 * H * W
+        per = a.info()["steps_per_launch"]
+        assert per == 2  # one attribute, one diffusion: fused step pairs
+        assert n == 20 // per and ms > 0 and bytes_per == 16.0 * H * W
         assert np.array_equal(a.download(), b.download())
+        assert np.array_equal(a.download(), O.field_step(O.fill_random(H, W), RATE, steps=20))
+
+
+def make_env_engine(gpu, monkeypatch, H, W, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    e = gpu.Engine(H, W)
+    for k in env:
+        monkeypatch.delenv(k)
+    return e
+
+
+@pytest.mark.parametrize("shape", [(3, 5), (37, 53), (130, 257), (257, 300), (64, 1000)])
+@pytest.mark.parametrize("steps", [1, 2, 5, 8])
+def test_fused_pairs_equal_single_steps(gpu, O, monkeypatch, shape, steps):
+    # two steps per pass (temporal blocking) against one step per pass and the oracle
+    H, W = shape
+    got = []
+    for env in ({"MM_FUSE": 0}, {}, {"MM_ROWS_PER_WAVE": 16}):
+        e = make_env_engine(gpu, monkeypatch, H, W, **env)
+        e.fill_random(0)
+        e.add_diffuse(0, 0.3)
+        e.run(steps)
+        got.append(e.download())
+        e.close()
+    want = O.field_step(O.fill_random(H, W), 0.3, steps=steps)
+    for g in got:
+        assert np.array_equal(g, want)
+
+
+@pytest.mark.parametrize("reduce_every", [1, 2, 3, 4])
+def test_fused_pairs_step_sums(gpu, O, reduce_every):
+    H, W, steps = 130, 257, 12
+    v = O.fill_random(H, W)
+    with gpu.Engine(H, W) as e:
+        e.upload(v)
+        e.add_diffuse(0, RATE)
+        e.run(steps, reduce_every)
+        hist = e.sums_history()
+        got = e.download()
+    want = []
+    ref = v
+    for k in range(1, steps + 1):
+        ref = O.field_step(ref, RATE)
+        if k % reduce_every == 0:
+            want.append(math.fsum(ref.ravel()))
+    assert np.array_equal(got, ref)
+    assert hist.shape == (len(want), 1)
+    for a, b in zip(hist[:, 0], want):
+        assert abs(a - b) <= 1e-12 * b
 
 
 C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),

@@ -16,9 +16,10 @@ import numpy as np  # noqa: E402
 import mpimodel as mm  # noqa: E402
 
 
-def make(H, W, th, variant):
+def make(H, W, th, variant, fuse):
     os.environ["MM_ROWS_PER_WAVE"] = str(th)
     os.environ["MM_KERNEL_VARIANT"] = str(variant)
+    os.environ["MM_FUSE"] = str(fuse)
     e = mm.Engine(H, W)
     e.fill_random(0)
     e.add_diffuse(0, 0.1)
@@ -40,31 +41,41 @@ def main():
     ap.add_argument("--variants", default="0,1,3")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--fuse", default="0,1")
     a = ap.parse_args()
     H = W = a.size
     ths = [int(x) for x in a.ths.split(",")]
     vs = [int(x) for x in a.variants.split(",")]
+    fs = [int(x) for x in a.fuse.split(",")]
     ref = None
     res = {}
     for rnd in range(a.rounds):
-        for th in ths:
-            for v in vs:
-                e = make(H, W, th, v)
-                e.run(10)
-                t, b = time_engine(e, a.steps)
-                res.setdefault((th, v), []).append(t)
-                if rnd == 0 and th == ths[0]:
-                    out = e.download()
-                    if ref is None:
-                        ref = out
-                    elif not np.array_equal(out, ref):
-                        print(json.dumps({"MISMATCH": [th, v]}), flush=True)
-                e.close()
-    for (th, v), ts in sorted(res.items(), key=lambda kv: statistics.median(kv[1])):
+        for f in fs:
+            for th in ths:
+                if f and th == 32:
+                    continue
+                for v in vs:
+                    if f and v == 3:
+                        continue
+                    e = make(H, W, th, v, f)
+                    e.run(10)
+                    t, b = time_engine(e, a.steps)
+                    per = e.info()["steps_per_launch"]
+                    res.setdefault((f, th, v, per), []).append(t)
+                    if rnd == 0:
+                        out = e.download()
+                        if ref is None:
+                            ref = out
+                        elif not np.array_equal(out, ref):
+                            print(json.dumps({"MISMATCH": [f, th, v]}), flush=True)
+                    e.close()
+    for (f, th, v, per), ts in sorted(res.items(), key=lambda kv: statistics.median(kv[1]) / kv[0][3]):
         med = statistics.median(ts)
-        print(json.dumps({"size": H, "th": th, "variant": v, "kernel_us_med": round(med * 1e3, 2),
-                          "kernel_us_min": round(min(ts) * 1e3, 2),
-                          "GBps": round(16.0 * H * W / (med * 1e-3) / 1e9, 1)}), flush=True)
+        print(json.dumps({"size": H, "fuse": f, "th": th, "variant": v,
+                          "us_per_step": round(med * 1e3 / per, 2),
+                          "GCUPS": round(H * W * per / (med * 1e-3) / 1e9, 1),
+                          "kernel_us_med": round(med * 1e3, 2),
+                          "GBps_per_launch": round(16.0 * H * W / (med * 1e-3) / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":
