@@ -119,8 +119,11 @@ int mm_device_count(int* n);
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
  * init loop (src/Model.hpp:154-157): device buffers are (h+4) x pitch fp64 per
  * attribute (two ghost rows above and below), two of them (Jacobi ping-pong).
- * Environment: MM_FUSE=0 disables the fused two-step kernel, MM_ROWS_PER_WAVE
- * (8/16/32) and MM_KERNEL_VARIANT (non-temporal policy) override tuning. */
+ * Environment: MM_FUSE=0 disables the fused two-step kernel, MM_GRAPH=0 the hipGraph
+ * replay, MM_ROWS_PER_WAVE (8/16/32), MM_ROWS_PER_WAVE2 (8/16, fused) and
+ * MM_KERNEL_VARIANT (non-temporal policy) override tuning; MM_SELF_HALO=1 with
+ * MM_HALO_RCCL and nranks == 1 makes the rank exchange border rows with itself
+ * (ghost rows outside the grid: exercises the RCCL path, result unchanged). */
 int mm_engine_create(const mm_desc* desc, mm_engine** out);
 int mm_engine_destroy(mm_engine* eng);
 int mm_engine_info(mm_engine* eng, mm_info* info);
@@ -165,6 +168,10 @@ int mm_clear_history(mm_engine* eng);
  * scalar halo messages src/Model.hpp:202-204 <-> :228-230 with whole rows. */
 int mm_halo_export(mm_engine* eng, double* top, double* bottom);
 int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
+
+/* Test/debug: copy nrows rows starting at local row row0 (owned rows are 0..h-1, ghost
+ * rows -2..-1 and h..h+1) of the current buffer of one attribute to host (W each). */
+int mm_debug_read_rows(mm_engine* eng, int attr, long long row0, long long nrows, double* host);
 
 /* Measurement: with timing on, mm_run records a HIP event pair around every
  * step-kernel launch on the stream it is launched on; mm_timing returns the

@@ -93,7 +93,9 @@ struct mm_engine {
     std::vector<FlowDesc> flows;
     std::vector<Pass> passes;
 
-    int th = 32;
+    int th = 8;       // rows per wave, one-step kernel
+    int th2 = 16;     // rows per wave, fused two-step kernel
+    bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
     double* partials = nullptr;
@@ -109,7 +111,8 @@ struct mm_engine {
     // graph cache: key = (parity, length, reduce_every)
     std::map<std::tuple<int, long long, long long>, hipGraphExec_t> graphs;
 
-    bool fuse_ok = true;  // MM_FUSE=0 disables the two-step kernel
+    bool fuse_ok = true;    // MM_FUSE=0 disables the two-step kernel
+    bool graphs_ok = true;  // MM_GRAPH=0 (or a refused capture) runs steps eagerly
 
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -167,11 +170,12 @@ int compile_passes(mm_engine* e) {
     return MM_OK;
 }
 
-// Waves for a row range of n rows.
-long long waves_for(const mm_engine* e, long long n) {
+// Waves for a row range of n rows at th rows per wave.
+long long waves_for(const mm_engine* e, long long n, int th) {
     if (n <= 0) return 0;
-    return e->nstrips * ((n + e->th - 1) / e->th);
+    return e->nstrips * ((n + th - 1) / th);
 }
+long long waves_for(const mm_engine* e, long long n) { return waves_for(e, n, e->th); }
 
 void fill_args(const mm_engine* e, const Pass& p, mm::PassArgs& A) {
     std::memset(&A, 0, sizeof A);
@@ -242,6 +246,17 @@ int halo_rccl(mm_engine* e, int depth) {
     MM_NCCL(ncclGroupStart());
     for (int a = 0; a < e->na; ++a) {
         double* b = e->buf[e->cur][a];
+        if (e->self_halo) {
+            // one rank, both neighbours itself: the first rows land in the bottom ghost
+            // rows and the last rows in the top ghost rows. Those ghost rows lie outside
+            // the grid, so the kernels never read them as cells: the exchange exercises
+            // the RCCL path without changing the result.
+            MM_NCCL(ncclSend(b, cnt, ncclDouble, 0, e->comm, e->s_comm));
+            MM_NCCL(ncclSend(b + (h - depth) * P, cnt, ncclDouble, 0, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b + h * P, cnt, ncclDouble, 0, e->comm, e->s_comm));
+            MM_NCCL(ncclRecv(b - depth * P, cnt, ncclDouble, 0, e->comm, e->s_comm));
+            continue;
+        }
         if (r > 0) {
             MM_NCCL(ncclSend(b, cnt, ncclDouble, r - 1, e->comm, e->s_comm));
             MM_NCCL(ncclRecv(b - depth * P, cnt, ncclDouble, r - 1, e->comm, e->s_comm));
@@ -263,15 +278,15 @@ int begin_halo(mm_engine* e, int depth) {
     return MM_OK;
 }
 
-// Rows [lo, hi) of the slab as range a, optional [lo2, hi2) as range b.
+// Rows [lo, hi) of the slab as range a, optional [lo2, hi2) as range b (A.th set).
 void set_ranges(const mm_engine* e, mm::PassArgs& A, long long lo, long long hi, long long lo2,
                 long long hi2) {
     A.ra0 = (int)lo;
     A.ra1 = (int)hi;
     A.rb0 = (int)lo2;
     A.rb1 = (int)hi2;
-    A.waves_a = waves_for(e, hi - lo);
-    A.waves_total = A.waves_a + waves_for(e, hi2 - lo2);
+    A.waves_a = waves_for(e, hi - lo, A.th);
+    A.waves_total = A.waves_a + waves_for(e, hi2 - lo2, A.th);
 }
 
 // One kernel pass over the slab, with the halo of `depth` rows exchanged first. With the
@@ -285,6 +300,7 @@ int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it)
     const int per_wave = fused ? entries : e->na;
     mm::PassArgs A;
     fill_args(e, p, A);
+    if (fused) A.th = e->th2;
     long long total_waves = 0;
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(begin_halo(e, depth));
@@ -341,7 +357,7 @@ bool fusable(const mm_engine* e) {
     const Pass& p = e->passes[0];
     if (!p.pre.empty() || !p.post.empty() || p.diffuse_mask != 1) return false;
     if (e->d.nranks > 1 && e->d.halo_mode != MM_HALO_RCCL) return false;
-    return e->th == 8 || e->th == 16;
+    return e->th2 == 8 || e->th2 == 16;
 }
 
 // Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
@@ -412,7 +428,7 @@ int choose_th(const mm_engine* e) {
 }
 
 int ensure_partials(mm_engine* e) {
-    long long need = waves_for(e, e->d.h) + 2 * waves_for(e, 1) + 16;
+    long long need = waves_for(e, e->d.h, 8) + 4 * waves_for(e, 2, 8) + 16;
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
@@ -496,7 +512,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         return fail(MM_ERR_INVALID, "mm_engine_create: bad rank/nranks");
     if (d.nranks == 1 && (d.x_init != 0 || d.h != d.H))
         return fail(MM_ERR_INVALID, "mm_engine_create: a single slab must own the whole grid");
-    if (d.halo_mode == MM_HALO_RCCL && d.nranks > 1 && !d.comm_id)
+    if (d.halo_mode == MM_HALO_RCCL && !d.comm_id)
         return fail(MM_ERR_INVALID, "mm_engine_create: MM_HALO_RCCL needs comm_id");
     if (d.nranks > 1 && d.halo_mode == MM_HALO_NONE)
         return fail(MM_ERR_INVALID, "mm_engine_create: nranks > 1 needs a halo mode");
@@ -510,7 +526,12 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->nstrips = (int)(e->pitch / mm::kStripCols);
     e->rows_alloc = d.h + 2 * mm::kGhost;
     if (const char* f = std::getenv("MM_FUSE")) e->fuse_ok = std::atoi(f) != 0;
+    if (const char* g = std::getenv("MM_GRAPH")) e->graphs_ok = std::atoi(g) != 0;
     e->th = choose_th(e);
+    if (const char* s2 = std::getenv("MM_ROWS_PER_WAVE2")) {
+        const int v = std::atoi(s2);
+        if (v == 8 || v == 16) e->th2 = v;
+    }
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
     // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
     e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
@@ -551,7 +572,9 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "sum scratch allocation failed"));
 
-    if (d.nranks > 1 && d.halo_mode == MM_HALO_RCCL) {
+    if (const char* sh = std::getenv("MM_SELF_HALO"))
+        e->self_halo = d.nranks == 1 && d.halo_mode == MM_HALO_RCCL && std::atoi(sh) != 0;
+    if ((d.nranks > 1 || e->self_halo) && d.halo_mode == MM_HALO_RCCL) {
         ncclUniqueId id;
         std::memcpy(&id, d.comm_id, sizeof id);
         ncclResult_t nr = ncclCommInitRank(&e->comm, d.nranks, id, d.rank);
@@ -591,7 +614,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->pitch = e->pitch;
     info->bytes_device = (long long)e->bytes;
     info->n_passes = (int)e->passes.size();
-    info->rows_per_wave = e->th;
+    info->rows_per_wave = fusable(e) ? e->th2 : e->th;
     info->waves_per_pass = waves_for(e, e->d.h);
     info->steps_done = e->steps_done;
     info->fused_attrs = e->na;
@@ -698,7 +721,7 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     const long long flips = fuse ? 1 : np;
     long long len = unit * ((flips % 2) ? 2 : 1);
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
-    if (len > 256 || nsteps < len) {
+    if (len > 256 || nsteps < len || !e->graphs_ok) {
         MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, false));
         e->steps_done += nsteps;
         return MM_OK;
@@ -706,7 +729,14 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     long long per = len;
     while (per < 16 && per * 2 <= nsteps) per *= 2;
     hipGraphExec_t g = nullptr;
-    MM_TRY(get_graph(e, per, reduce_every, &g));
+    if (get_graph(e, per, reduce_every, &g) != MM_OK) {
+        // stream capture refused (e.g. by the RCCL build): run the same steps eagerly
+        (void)hipGetLastError();
+        e->graphs_ok = false;
+        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, false));
+        e->steps_done += nsteps;
+        return MM_OK;
+    }
     long long done = 0;
     for (; done + per <= nsteps; done += per) MM_HIP(hipGraphLaunch(g, e->s_comp));
     if (done < nsteps) MM_TRY(enqueue_steps(e, done + 1, nsteps - done, reduce_every, false));
@@ -783,6 +813,19 @@ int mm_halo_import(mm_engine* e, const double* top, const double* bottom) {
             MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + h * P, bottom + a * W,
                                   sizeof(double) * W, hipMemcpyHostToDevice, e->s_comp));
     }
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_debug_read_rows(mm_engine* e, int attr, long long row0, long long nrows, double* host) {
+    if (!e || !host || attr < 0 || attr >= e->na || nrows < 0 || row0 < -mm::kGhost ||
+        row0 + nrows > e->d.h + mm::kGhost)
+        return fail(MM_ERR_INVALID, "mm_debug_read_rows: rows outside the slab + ghost rows");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    MM_HIP(hipMemcpy2DAsync(host, sizeof(double) * e->d.W, e->buf[e->cur][attr] + row0 * e->pitch,
+                            sizeof(double) * e->pitch, sizeof(double) * e->d.W, nrows,
+                            hipMemcpyDeviceToHost, e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comp));
     return MM_OK;
 }

@@ -30,7 +30,8 @@ EXPORTS = [
     "mm_comm_id_create", "mm_device_count", "mm_engine_create", "mm_engine_destroy",
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
     "mm_point_apply", "mm_run", "mm_synchronize", "mm_sums", "mm_sums_history",
-    "mm_clear_history", "mm_halo_export", "mm_halo_import", "mm_set_timing", "mm_timing",
+    "mm_clear_history", "mm_halo_export", "mm_halo_import", "mm_debug_read_rows",
+    "mm_set_timing", "mm_timing",
 ]
 
 
@@ -93,6 +94,7 @@ def lib():
             "mm_clear_history": (I, [P]),
             "mm_halo_export": (I, [P, P, P]),
             "mm_halo_import": (I, [P, P, P]),
+            "mm_debug_read_rows": (I, [P, I, LL, LL, P]),
             "mm_set_timing": (I, [P, I]),
             "mm_timing": (I, [P, pLL, ctypes.POINTER(D), ctypes.POINTER(D)]),
         }
@@ -250,6 +252,11 @@ class Engine:
         t = None if top is None else np.ascontiguousarray(top, dtype=np.float64)
         b = None if bottom is None else np.ascontiguousarray(bottom, dtype=np.float64)
         check(lib().mm_halo_import(self.ptr, _dptr(t), _dptr(b)))
+
+    def read_rows(self, row0, nrows, attr=0):
+        out = np.empty((nrows, self.W), dtype=np.float64)
+        check(lib().mm_debug_read_rows(self.ptr, attr, row0, nrows, _dptr(out)))
+        return out
 
     def set_timing(self, on):
         check(lib().mm_set_timing(self.ptr, 1 if on else 0))

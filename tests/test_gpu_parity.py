@@ -289,3 +289,56 @@ def test_engine_rejects_bad_shapes(gpu):
             e.run(1)  # no flow
         with pytest.raises(gpu.MMError):
             e.point_apply(8, 0, 1.0, 0.1)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("graph", [0, 1])
+def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, fuse, graph):
+    # The RCCL halo path on one GPU: one rank whose two neighbours are itself
+    # (MM_SELF_HALO). Border rows go through ncclSend/ncclRecv on the comm stream, the
+    # interior rows run meanwhile, the border rows after the event join -- eagerly and
+    # captured in a hipGraph. The received rows land in ghost rows outside the grid, so
+    # the cells must still match the oracle bit for bit.
+    H, W = 64, 300
+    depth = 2 if fuse else 1
+    steps = 2 * depth  # two passes: afterwards the current buffer's ghost rows hold the
+                       # rows exchanged in the first pass (the initial state's)
+    for k, v in {"MM_SELF_HALO": 1, "MM_FUSE": fuse, "MM_GRAPH": graph}.items():
+        monkeypatch.setenv(k, str(v))
+    e = gpu.Engine(H, W, halo_mode=gpu.MM_HALO_RCCL, comm_id_bytes=gpu.comm_id())
+    for k in ("MM_SELF_HALO", "MM_FUSE", "MM_GRAPH"):
+        monkeypatch.delenv(k)
+    v0 = O.fill_random(H, W)
+    e.fill_random(0)
+    e.add_diffuse(0, RATE)
+    assert e.info()["steps_per_launch"] == (2 if fuse else 1)
+    e.run(steps, reduce_every=1)
+    got = e.download()
+    top = e.read_rows(-depth, depth)
+    bot = e.read_rows(H, depth)
+    hist = e.sums_history()
+    e.close()
+    ref = v0
+    sums = []
+    for _ in range(steps):
+        ref = O.field_step(ref, RATE)
+        sums.append(math.fsum(ref.ravel()))
+    assert np.array_equal(got, ref)
+    assert np.array_equal(bot, v0[:depth])        # first rows -> bottom ghost rows
+    assert np.array_equal(top, v0[H - depth:])    # last rows -> top ghost rows
+    for a, b in zip(hist[:, 0], sums):
+        assert abs(a - b) <= 1e-12 * b
+
+
+def test_rccl_halo_path_many_steps(gpu, O, monkeypatch):
+    # graph replay of RCCL calls over many steps, odd step count (fused pairs + one single)
+    monkeypatch.setenv("MM_SELF_HALO", "1")
+    H, W, steps = 200, 520, 25
+    e = gpu.Engine(H, W, halo_mode=gpu.MM_HALO_RCCL, comm_id_bytes=gpu.comm_id())
+    monkeypatch.delenv("MM_SELF_HALO")
+    e.fill_random(0)
+    e.add_diffuse(0, RATE)
+    e.run(steps)
+    got = e.download()
+    e.close()
+    assert np.array_equal(got, O.field_step(O.fill_random(H, W), RATE, steps=steps))
