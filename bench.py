@@ -32,6 +32,11 @@ sys.path.insert(0, os.path.join(REPO, "mpi-model_amd"))
 
 import mpimodel as mm  # noqa: E402
 
+# Load the engine (and with it ROCm's libamdhip64 / librccl) BEFORE torch: torch bundles
+# its own HIP runtime and librccl.so.1 with the same sonames, and whichever is loaded
+# first is used by the whole process. The engine is built against /opt/rocm.
+mm.lib()
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 RATE = 0.1             # src/Main.cpp:33
 
@@ -59,6 +64,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--self-halo", action="store_true",
+                    help="N=1 only: run the RCCL halo path against itself (MM_SELF_HALO) to "
+                         "price the exchange + interior/border split")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample length (oracle port, rank 0, N=1)")
     return ap.parse_args()
@@ -116,6 +124,10 @@ def main():
         dist.broadcast_object_list(ids, src=0)
         eng = mm.Engine(H, W, x0, h, n_attr=wl["n_attr"], device=local, rank=rank, nranks=N,
                         halo_mode=mm.MM_HALO_RCCL, comm_id_bytes=ids[0])
+    elif args.self_halo:
+        os.environ["MM_SELF_HALO"] = "1"
+        eng = mm.Engine(H, W, n_attr=wl["n_attr"], device=local, halo_mode=mm.MM_HALO_RCCL,
+                        comm_id_bytes=mm.comm_id())
     else:
         eng = mm.Engine(H, W, n_attr=wl["n_attr"], device=local)
     torch.cuda.set_device(local)
@@ -200,7 +212,8 @@ def main():
                        "path": "hipGraph replay, " + ("two fused steps per kernel pass"
                                                       if fused else "one step per pass"),
                        "rows_per_gpu": h, "n_attr": na, "rate": RATE,
-                       "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else ""),
+                       "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else "")
+                       + (" (self-halo: RCCL exchange with itself)" if args.self_halo else ""),
                        "passes_per_step": info["n_passes"],
                        "rows_per_wave": info["rows_per_wave"]},
             "roofline": {

@@ -575,6 +575,17 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* sh = std::getenv("MM_SELF_HALO"))
         e->self_halo = d.nranks == 1 && d.halo_mode == MM_HALO_RCCL && std::atoi(sh) != 0;
     if ((d.nranks > 1 || e->self_halo) && d.halo_mode == MM_HALO_RCCL) {
+        // a process that loaded another librccl.so.1 first (PyTorch bundles one) would
+        // run this code against a different RCCL: refuse instead of crashing later
+        int v = 0;
+        if (ncclGetVersion(&v) != ncclSuccess || v != NCCL_VERSION_CODE) {
+            char msg[160];
+            std::snprintf(msg, sizeof msg,
+                          "RCCL %d loaded, engine built against %d: load libmpimodel_hip.so "
+                          "before any library that bundles its own librccl (e.g. torch)",
+                          v, NCCL_VERSION_CODE);
+            return cleanup(fail(MM_ERR_RCCL, msg));
+        }
         ncclUniqueId id;
         std::memcpy(&id, d.comm_id, sizeof id);
         ncclResult_t nr = ncclCommInitRank(&e->comm, d.nranks, id, d.rank);
