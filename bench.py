@@ -11,8 +11,8 @@ workload: default "c2" = BASELINE.json configs[1]: 4096 x 4096 fp64 cells per GP
           chained transfers + 4 diffusions, per-step sums).
 step    : one pass of the flow over the whole grid (all passes of the program).
 timing  : W untimed warmup steps, then exactly K steps on the production path (hipGraph
-          replay of fused step pairs) bracketed by a barrier and torch.cuda.synchronize()
-          on both sides; the max over ranks is reported. Inputs are resident in HBM
+          replay of fused step pairs) bracketed by a barrier and a device-wide
+          synchronize (hipDeviceSynchronize) on both sides; the max over ranks is reported. Inputs are resident in HBM
           (generated on the device) before timing. Then the same K steps again, launched
           eagerly with a HIP event pair around every step kernel on its own stream: the
           kernel's average duration for the roofline object.
@@ -32,9 +32,13 @@ sys.path.insert(0, os.path.join(REPO, "mpi-model_amd"))
 
 import mpimodel as mm  # noqa: E402
 
-# Load the engine (and with it ROCm's libamdhip64 / librccl) BEFORE torch: torch bundles
-# its own HIP runtime and librccl.so.1 with the same sonames, and whichever is loaded
-# first is used by the whole process. The engine is built against /opt/rocm.
+# Load the engine (and with it ROCm 7.2's libamdhip64 / librccl) BEFORE torch: torch
+# bundles its own HIP 7.0 runtime and librccl.so.1 under the same sonames, and whichever
+# is loaded first serves the whole process. With torch's RCCL the engine's halo path
+# crashes; with ROCm's runtime torch.cuda sees no device. So the process runs on ROCm
+# 7.2 only, torch is used for the launcher and the gloo control plane, and the device
+# synchronize around the timed region is hipDeviceSynchronize via the engine
+# (the same operation torch.cuda.synchronize performs).
 mm.lib()
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
@@ -130,7 +134,7 @@ def main():
                         comm_id_bytes=mm.comm_id())
     else:
         eng = mm.Engine(H, W, n_attr=wl["n_attr"], device=local)
-    torch.cuda.set_device(local)
+    sync = lambda: mm.device_synchronize(local)  # noqa: E731
 
     na = wl["n_attr"]
     for a in range(na):
@@ -161,11 +165,11 @@ def main():
     # timed region: the production path
     if N > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     eng.run(args.steps, reduce_every)
     eng.synchronize()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     if N > 1:
         dist.barrier()

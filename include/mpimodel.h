@@ -114,6 +114,8 @@ int mm_comm_id_size(void);
 int mm_comm_id_create(void* out, int len);
 
 int mm_device_count(int* n);
+/* hipDeviceSynchronize on one device: every stream of every engine on it. */
+int mm_device_synchronize(int device);
 
 /* ---- engine ------------------------------------------------------------- */
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the

@@ -494,6 +494,12 @@ int mm_comm_id_create(void* out, int len) {
     return MM_OK;
 }
 
+int mm_device_synchronize(int device) {
+    MM_HIP(hipSetDevice(device));
+    MM_HIP(hipDeviceSynchronize());
+    return MM_OK;
+}
+
 int mm_device_count(int* n) {
     if (!n) return fail(MM_ERR_INVALID, "mm_device_count: null");
     MM_HIP(hipGetDeviceCount(n));

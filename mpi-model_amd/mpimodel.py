@@ -27,7 +27,7 @@ SEED = 0x4D50494D
 EXPORTS = [
     "mm_abi_version", "mm_last_error", "mm_step_count", "mm_partition_reference",
     "mm_owner_reference", "mm_partition_rows", "mm_neighbor_count", "mm_comm_id_size",
-    "mm_comm_id_create", "mm_device_count", "mm_engine_create", "mm_engine_destroy",
+    "mm_comm_id_create", "mm_device_count", "mm_device_synchronize", "mm_engine_create", "mm_engine_destroy",
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
     "mm_point_apply", "mm_run", "mm_synchronize", "mm_sums", "mm_sums_history",
     "mm_clear_history", "mm_halo_export", "mm_halo_import", "mm_debug_read_rows",
@@ -78,6 +78,7 @@ def lib():
             "mm_comm_id_size": (I, []),
             "mm_comm_id_create": (I, [P, I]),
             "mm_device_count": (I, [pI]),
+            "mm_device_synchronize": (I, [I]),
             "mm_engine_create": (I, [ctypes.POINTER(Desc), ctypes.POINTER(P)]),
             "mm_engine_destroy": (I, [P]),
             "mm_engine_info": (I, [P, ctypes.POINTER(Info)]),
@@ -148,6 +149,10 @@ def comm_id():
     buf = ctypes.create_string_buffer(n)
     check(lib().mm_comm_id_create(buf, n))
     return buf.raw
+
+
+def device_synchronize(device=0):
+    check(lib().mm_device_synchronize(device))
 
 
 def device_count():

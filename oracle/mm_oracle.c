@@ -130,7 +130,9 @@ static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
         }
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
-        for (long long y = 0; y < W; ++y) {
+        if (v == NULL) {  /* output row outside the grid (or the slab): no cells, zeros */
+            for (long long y = 0; y < W; ++y) o[y] = 0.0;
+        } else for (long long y = 0; y < W; ++y) {
             int cnt = or_neighbor_count(H, W, x, y);
             double out = cnt > 0 ? rate * v[y] : 0.0;
             double nb = (c3[y] + c3[y + 2]) + p[y];

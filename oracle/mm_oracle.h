@@ -67,7 +67,7 @@ void or_field_step(long long H, long long W, const double* v, double* vout, doub
 
 /* One generalised step on a row slab with ghost rows: vg has (h+2) rows of W,
  * row 0 = global row x_init-1, row h+1 = global row x_init+h (ignored when
- * outside the grid). Writes h rows to vout. */
+ * outside the grid). Writes h rows to vout; rows outside the grid are written as 0. */
 void or_field_step_slab(long long H, long long W, long long x_init, long long h,
                         const double* vg, double* vout, double rate);
 

@@ -7,13 +7,14 @@ averaged; FETCH_SIZE doubled, the gfx950 correction of MI355X_MICROARCH.md 'HBM'
 (it counts 64 B per 128-B request of a wide coalesced stream).
 """
 import csv
+import re
 import glob
 import json
 import os
 import statistics
 import sys
 
-KERNEL = "mm_pass_kernel"
+KERNEL_RE = re.compile(r"mm_pass2?_kernel")
 
 
 def rows(pattern):
@@ -27,17 +28,23 @@ def rows(pattern):
 def main():
     d, wl = sys.argv[1], sys.argv[2]
     res = {"workload": wl}
-    stats = rows(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
-    for r in stats:
-        if KERNEL in r.get("Name", ""):
-            res["kernel_name"] = r["Name"][:120]
-            res["calls"] = int(r["Calls"])
-            res["avg_us"] = float(r["AverageNs"]) / 1e3
-            res["min_us"] = float(r["MinNs"]) / 1e3
-            res["max_us"] = float(r["MaxNs"]) / 1e3
+    stats = [r for r in rows(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
+             if KERNEL_RE.search(r.get("Name", ""))]
+    # the dominant step kernel: largest total time
+    stats.sort(key=lambda r: float(r["TotalDurationNs"]), reverse=True)
+    name = None
+    if stats:
+        r = stats[0]
+        name = r["Name"]
+        res["kernel_name"] = name[:120]
+        res["calls"] = int(r["Calls"])
+        res["avg_us"] = float(r["AverageNs"]) / 1e3
+        res["min_us"] = float(r["MinNs"]) / 1e3
+        res["max_us"] = float(r["MaxNs"]) / 1e3
+        res["share_of_gpu_time"] = float(r.get("Percentage", 0.0))
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
-                if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter]
+                if name and r.get("Kernel_Name", "") == name and r.get("Counter_Name") == counter]
         if vals:
             res[counter + "_KB_avg"] = statistics.mean(vals)
             res[counter + "_dispatches"] = len(vals)
