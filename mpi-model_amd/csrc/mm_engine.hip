@@ -87,6 +87,8 @@ struct mm_engine {
     int cur = 0;
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    hipEvent_t ev_comp_mark = nullptr, ev_comm_done = nullptr;
+    bool comm_live = false;  // border work of this run is pending on the comm stream
     ncclComm_t comm = nullptr;
     bool split = false;  // interior / border split (RCCL halo)
 
@@ -303,19 +305,42 @@ int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it)
     if (fused) A.th = e->th2;
     long long total_waves = 0;
     if (e->split && h >= 2 * depth + 1) {
-        MM_TRY(begin_halo(e, depth));
+        // Two streams per pass, joined by events:
+        //   comm:    halo exchange k (right after border k-1) -> [after interior k-1] border k
+        //   compute: [after border k-1] interior k
+        // so the exchange and the border rows run beside the interior kernels. Interior k
+        // reads rows written by border k-1; border k reads rows written by interior k-1
+        // and writes rows interior k-1 read; ghost rows are only touched on comm; the
+        // rows an exchange sends were written by the border kernel before it.
+        if (e->comm_live) {
+            // interior k reads the rows border k-1 wrote
+            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+        } else {
+            // first split pass of the run: the exchange follows all earlier compute work
+            MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
+        }
+        // the exchange needs only border k-1 (same stream): it overlaps interior k-1
+        MM_TRY(halo_rccl(e, depth));
+        // border k reads rows interior k-1 wrote (and reuses the partials finalize k-1 read)
+        MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+        MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
         set_ranges(e, A, depth, h - depth, 0, 0);
+        const long long interior_waves = A.waves_total;
+        mm::PassArgs B = A;
+        B.th = fused ? 2 : 1;  // border: short row blocks, the launch is latency-bound
+        set_ranges(e, B, 0, depth, h - depth, h);
+        B.partial_base = interior_waves;
+        if (fused)
+            MM_HIP(mm::launch_pass2(red, B, e->s_comm, e->variant));
+        else
+            MM_HIP(mm::launch_pass(e->na, red != 0, B, e->s_comm, e->variant));
+        MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
+        e->comm_live = true;
         A.partial_base = 0;
         MM_TRY(launch_timed(e, fused, red, A, h - 2 * depth, time_it));
-        total_waves = A.waves_total;
-        MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
-        set_ranges(e, A, 0, depth, h - depth, h);
-        A.partial_base = total_waves;
-        if (fused)
-            MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
-        else
-            MM_HIP(mm::launch_pass(e->na, red != 0, A, e->s_comp, e->variant));
-        total_waves += A.waves_total;
+        total_waves = interior_waves + B.waves_total;
+        if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
         if (e->split) {  // slab too thin to split: exchange first, then one launch
             MM_TRY(begin_halo(e, depth));
@@ -376,6 +401,11 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
             s += 1;
         }
     }
+    // the compute stream is the tail of every run (and of every captured graph)
+    if (e->comm_live) {
+        MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+        e->comm_live = false;
+    }
     return MM_OK;
 }
 
@@ -428,7 +458,7 @@ int choose_th(const mm_engine* e) {
 }
 
 int ensure_partials(mm_engine* e) {
-    long long need = waves_for(e, e->d.h, 8) + 4 * waves_for(e, 2, 8) + 16;
+    long long need = waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16;
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
@@ -564,7 +594,9 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_halo, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&e->ev_halo, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_comp_mark, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_comm_done, hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(MM_ERR_HIP, "stream/event creation failed"));
 
     int rc = ensure_partials(e);
@@ -614,6 +646,8 @@ int mm_engine_destroy(mm_engine* e) {
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
     if (e->ev_halo) (void)hipEventDestroy(e->ev_halo);
+    if (e->ev_comp_mark) (void)hipEventDestroy(e->ev_comp_mark);
+    if (e->ev_comm_done) (void)hipEventDestroy(e->ev_comm_done);
     if (e->s_comp) (void)hipStreamDestroy(e->s_comp);
     if (e->s_comm) (void)hipStreamDestroy(e->s_comm);
     if (e->base) (void)hipFree(e->base);

@@ -667,6 +667,7 @@ hipError_t launch_pass_na<1>(bool reduce, const PassArgs& a, hipStream_t s, int 
         return launch_c<1, 8, 8, 0, true>(reduce, a, s);
     }
     switch (a.th) {
+        case 1: return launch_c<1, 1, 1, 0, false>(reduce, a, s);  // border row of a split pass
         case 8: return launch_one<8>(reduce, a, s, variant);
         case 16: return launch_one<16>(reduce, a, s, variant);
         case 32: return launch_one<32>(reduce, a, s, variant);
@@ -701,7 +702,9 @@ hipError_t launch2_v(int red, const PassArgs& a, hipStream_t s) {
 
 hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant) {
     if (a.waves_total <= 0) return hipSuccess;
-    // variant: non-temporal policy (0 none, 1 stores); rows per wave a.th in {8, 16}
+    // variant: non-temporal policy (0 none, 1 stores); rows per wave a.th in {8, 16},
+    // 2 for the border rows of a halo-split pass (short chains for a latency-bound launch)
+    if (a.th == 2) return launch2_v<2, 4, 0>(red, a, s);
     if (a.th == 16) return variant == 1 ? launch2_v<16, 8, 1>(red, a, s) : launch2_v<16, 8, 0>(red, a, s);
     if (a.th != 8) return hipErrorInvalidValue;
     return variant == 1 ? launch2_v<8, 8, 1>(red, a, s) : launch2_v<8, 8, 0>(red, a, s);

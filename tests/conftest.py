@@ -12,6 +12,16 @@ for p in (PKG, ORACLE, REPO):
         sys.path.insert(0, p)
 
 
+# Load the engine (ROCm's HIP runtime and librccl) before any test module imports torch,
+# which bundles its own librccl.so.1 / libamdhip64 under the same sonames (bench.py does
+# the same). Loading needs no GPU.
+try:
+    import mpimodel as _mm
+    _mm.lib()
+except Exception:  # library not built yet: the tests that need it fail on their own
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
 
