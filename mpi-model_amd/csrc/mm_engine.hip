@@ -96,7 +96,11 @@ struct mm_engine {
     std::vector<Pass> passes;
 
     int th = 8;       // rows per wave, one-step kernel
-    int th2 = 16;     // rows per wave, fused two-step kernel
+    int th2 = 16;     // rows per wave, fused two-step kernel (MM_PASSK=0)
+    bool passk = true;  // K-step overlapped-strip kernel (mm_passk_kernel) for fusable programs
+    int kpass = 4;      // steps per pass of mm_passk_kernel (MM_STEPS_PER_PASS, 1..4)
+    int thk = 32;       // rows per wave of mm_passk_kernel (MM_ROWS_PER_WAVE_K: 16 / 32)
+    int xcd = 1;        // XCD-contiguous block order for mm_passk_kernel (MM_XCD_REMAP)
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -172,11 +176,12 @@ int compile_passes(mm_engine* e) {
     return MM_OK;
 }
 
-// Waves for a row range of n rows at th rows per wave.
-long long waves_for(const mm_engine* e, long long n, int th) {
+// Waves for a row range of n rows at th rows per wave (nstrips column strips).
+long long waves_for(long long nstrips, long long n, int th) {
     if (n <= 0) return 0;
-    return e->nstrips * ((n + th - 1) / th);
+    return nstrips * ((n + th - 1) / th);
 }
+long long waves_for(const mm_engine* e, long long n, int th) { return waves_for(e->nstrips, n, th); }
 long long waves_for(const mm_engine* e, long long n) { return waves_for(e, n, e->th); }
 
 void fill_args(const mm_engine* e, const Pass& p, mm::PassArgs& A) {
@@ -217,10 +222,11 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
-// Launch a pass (fused == 0) or a fused two-step pass (fused == 1, `red` = its RED mode)
-// covering `rows` rows, with an event pair around it when timing.
+// Launch a pass (fused == 0), a fused two-step pass (fused == 1, `red` = its RED mode)
+// or, with kpass > 0, a K-step pass (mm_passk_kernel, red != 0: per-level sums) covering
+// `rows` rows, with an event pair around it when timing.
 int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long long rows,
-                 bool time_it) {
+                 bool time_it, int kpass = 0) {
     hipEvent_t a = nullptr, b = nullptr;
     if (time_it) {
         a = next_event(e);
@@ -230,12 +236,19 @@ int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long 
         e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * (fused ? 1 : e->na);
         MM_HIP(hipEventRecord(a, e->s_comp));
     }
-    if (fused)
+    if (kpass > 0)
+        MM_HIP(mm::launch_passk(kpass, red != 0, A, e->s_comp, e->variant));
+    else if (fused)
         MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
     else
         MM_HIP(mm::launch_pass(e->na, red != 0, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
     return MM_OK;
+}
+
+long long nstrips_k(const mm_engine* e, int k) {
+    const int oc = mm::passk_out_cols(k);
+    return (e->d.W + oc - 1) / oc;
 }
 
 // Border-row exchange with both neighbours in one RCCL group: the first / last `depth`
@@ -283,12 +296,13 @@ int begin_halo(mm_engine* e, int depth) {
 // Rows [lo, hi) of the slab as range a, optional [lo2, hi2) as range b (A.th set).
 void set_ranges(const mm_engine* e, mm::PassArgs& A, long long lo, long long hi, long long lo2,
                 long long hi2) {
+    (void)e;
     A.ra0 = (int)lo;
     A.ra1 = (int)hi;
     A.rb0 = (int)lo2;
     A.rb1 = (int)hi2;
-    A.waves_a = waves_for(e, hi - lo, A.th);
-    A.waves_total = A.waves_a + waves_for(e, hi2 - lo2, A.th);
+    A.waves_a = waves_for(A.nstrips, hi - lo, A.th);
+    A.waves_total = A.waves_a + waves_for(A.nstrips, hi2 - lo2, A.th);
 }
 
 // One kernel pass over the slab, with the halo of `depth` rows exchanged first. With the
@@ -359,6 +373,60 @@ int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it)
     return MM_OK;
 }
 
+// k (1..4) fused steps in one mm_passk_kernel pass; bit j of `mask`: append the sum after
+// step j+1 of the pass to the history. Same two-stream structure as enqueue_pass, with a
+// k-row halo (every k steps) and 4-row blocks for the border launch.
+int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
+    const long long h = e->d.h;
+    const int depth = k;
+    const bool red = mask != 0;
+    mm::PassArgs A;
+    fill_args(e, e->passes[0], A);
+    A.th = e->thk;
+    A.nstrips = (int)nstrips_k(e, k);
+    A.xcd_remap = e->xcd;
+    long long total_waves = 0;
+    if (e->split && h >= 2 * depth + 1) {
+        if (e->comm_live) {
+            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+        } else {
+            MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
+        }
+        MM_TRY(halo_rccl(e, depth));
+        MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+        MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
+        set_ranges(e, A, depth, h - depth, 0, 0);
+        const long long interior_waves = A.waves_total;
+        mm::PassArgs B = A;
+        B.th = 4;  // border: short row blocks, the launch is latency-bound
+        B.xcd_remap = 0;
+        set_ranges(e, B, 0, depth, h - depth, h);
+        B.partial_base = interior_waves;
+        MM_HIP(mm::launch_passk(k, red, B, e->s_comm, 0));
+        MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
+        e->comm_live = true;
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, true, red, A, h - 2 * depth, time_it, k));
+        total_waves = interior_waves + B.waves_total;
+        if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+    } else {
+        if (e->split) {
+            MM_TRY(begin_halo(e, depth));
+            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
+        }
+        set_ranges(e, A, 0, h, 0, 0);
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, true, red, A, h, time_it, k));
+        total_waves = A.waves_total;
+    }
+    if (red)
+        MM_HIP(mm::launch_finalize_levels(e->partials, total_waves, k, mask, e->hist, e->hist_n,
+                                          e->hist_cap, e->s_comp));
+    e->cur ^= 1;
+    return MM_OK;
+}
+
 // One step (all passes); reduce: append the per-attribute sums to the history.
 int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
     const int np = (int)e->passes.size();
@@ -385,6 +453,13 @@ bool fusable(const mm_engine* e) {
     return e->th2 == 8 || e->th2 == 16;
 }
 
+// Steps one kernel pass advances: kpass with the K-step kernel, 2 with the fused pair
+// kernel, 1 otherwise.
+int steps_per_launch(const mm_engine* e) {
+    if (!fusable(e)) return 1;
+    return e->passk ? e->kpass : 2;
+}
+
 // Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
 int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_every,
                   bool time_it) {
@@ -392,6 +467,21 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
     long long s = first;
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
+    if (fuse && e->passk) {
+        while (s < end) {
+            const int k = (int)std::min<long long>(e->kpass, end - s);
+            int mask = 0;
+            for (int j = 0; j < k; ++j)
+                if (red(s + j)) mask |= 1 << j;
+            MM_TRY(enqueue_passk(e, k, mask, time_it));
+            s += k;
+        }
+        if (e->comm_live) {
+            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+            e->comm_live = false;
+        }
+        return MM_OK;
+    }
     while (s < end) {
         if (fuse && s + 1 < end) {
             MM_TRY(enqueue_pair(e, red(s), red(s + 1), time_it));
@@ -459,6 +549,10 @@ int choose_th(const mm_engine* e) {
 
 int ensure_partials(mm_engine* e) {
     long long need = waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16;
+    // mm_passk_kernel: at most ceil(W/120) strips x (h/16 + 2 border blocks) waves, and
+    // kMaxSteps (= kMaxAttr) partials per wave
+    need = std::max(need, waves_for(nstrips_k(e, mm::kMaxSteps), e->d.h, 16) +
+                              2 * nstrips_k(e, mm::kMaxSteps) + 16);
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
@@ -568,6 +662,16 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         const int v = std::atoi(s2);
         if (v == 8 || v == 16) e->th2 = v;
     }
+    if (const char* p = std::getenv("MM_PASSK")) e->passk = std::atoi(p) != 0;
+    if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
+        const int v = std::atoi(k);
+        if (v >= 1 && v <= mm::kMaxSteps) e->kpass = v;
+    }
+    if (const char* t = std::getenv("MM_ROWS_PER_WAVE_K")) {
+        const int v = std::atoi(t);
+        if (v == 16 || v == 32) e->thk = v;
+    }
+    if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
     // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
     e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
@@ -665,11 +769,13 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->pitch = e->pitch;
     info->bytes_device = (long long)e->bytes;
     info->n_passes = (int)e->passes.size();
-    info->rows_per_wave = fusable(e) ? e->th2 : e->th;
-    info->waves_per_pass = waves_for(e, e->d.h);
+    const int spl = steps_per_launch(e);
+    const bool k = fusable(e) && e->passk;
+    info->rows_per_wave = k ? e->thk : (fusable(e) ? e->th2 : e->th);
+    info->waves_per_pass = k ? waves_for(nstrips_k(e, spl), e->d.h, e->thk) : waves_for(e, e->d.h);
     info->steps_done = e->steps_done;
     info->fused_attrs = e->na;
-    info->steps_per_launch = fusable(e) ? 2 : 1;
+    info->steps_per_launch = spl;
     return MM_OK;
 }
 
@@ -768,7 +874,7 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     // Replay a graph of `per` steps: a whole number of fused pairs, an even number of
     // buffer flips (so the captured pointers are valid again) and of reduction periods.
     const bool fuse = fusable(e);
-    const long long unit = fuse ? 2 : 1;
+    const long long unit = steps_per_launch(e);
     const long long flips = fuse ? 1 : np;
     long long len = unit * ((flips % 2) ? 2 : 1);
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;

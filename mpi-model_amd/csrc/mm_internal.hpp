@@ -11,7 +11,8 @@ constexpr int kMaxChain = 8;    // elementwise transfers before / after a pass's
 constexpr int kStripCols = 128; // columns per wave: 64 lanes x double2 (16 B per lane)
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
-constexpr int kGhost = 2;       // ghost rows above and below a slab (two fused steps need 2)
+constexpr int kMaxSteps = 4;    // fused steps per pass of mm_passk_kernel
+constexpr int kGhost = kMaxSteps;  // ghost rows above and below a slab (K fused steps need K)
 
 // One fused Jacobi pass over a row slab. Every buffer pointer points at owned row 0;
 // rows -kGhost..-1 and h..h+kGhost-1 are ghost rows; local row r is global x_init+r.
@@ -35,8 +36,9 @@ struct PassArgs {
     signed char pre_a[kMaxChain], pre_b[kMaxChain];
     signed char post_a[kMaxChain], post_b[kMaxChain];
     double pre_r[kMaxChain], post_r[kMaxChain];
-    double* partials;       // REDUCE: [partial_base + wave][NA]
+    double* partials;       // REDUCE: [partial_base + wave][NA] (mm_passk_kernel: [..][K])
     long long partial_base;
+    int xcd_remap;          // mm_passk_kernel: XCD-contiguous block order (grid padded to 8)
 };
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
@@ -44,6 +46,16 @@ hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, in
 // Two fused steps of a single-attribute, single-diffusion program (mm_pass2_kernel).
 // red: 0 no sums, 1 second step's sums (partials[wave]), 2 both (partials[wave][2]).
 hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant);
+// K (1..4) fused steps of a single-attribute, single-diffusion program on overlapped
+// strips (mm_passk_kernel, mm_kernels_k.hip); a.th in {4, 16, 32}, a.nstrips =
+// ceil(W / passk_out_cols(k)). red: every level's sums into partials[wave][k].
+hipError_t launch_passk(int k, bool red, const PassArgs& a, hipStream_t s, int variant);
+int passk_out_cols(int k);
+// Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k],
+// each summed in a fixed order, to the history.
+hipError_t launch_finalize_levels(const double* partials, long long n, int k, int mask,
+                                  double* hist, unsigned long long* hist_n, long long cap,
+                                  hipStream_t s);
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
                        long long h, int mode, double value, unsigned long long seed, hipStream_t s);
 hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,

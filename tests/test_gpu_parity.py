@@ -153,7 +153,7 @@ def test_timed_eager_path_equals_graph_path(gpu, O):
         b.run(20)
         n, ms, bytes_per = a.timing()
         per = a.info()["steps_per_launch"]
-        assert per == 2  # one attribute, one diffusion: fused step pairs
+        assert per == 4  # one attribute, one diffusion: K = 4 fused steps per pass
         assert n == 20 // per and ms > 0 and bytes_per == 16.0 * H * W
         assert np.array_equal(a.download(), b.download())
         assert np.array_equal(a.download(), O.field_step(O.fill_random(H, W), RATE, steps=20))
@@ -168,34 +168,56 @@ def make_env_engine(gpu, monkeypatch, H, W, **env):
     return e
 
 
-@pytest.mark.parametrize("shape", [(3, 5), (37, 53), (130, 257), (257, 300), (64, 1000)])
-@pytest.mark.parametrize("steps", [1, 2, 5, 8])
-def test_fused_pairs_equal_single_steps(gpu, O, monkeypatch, shape, steps):
-    # two steps per pass (temporal blocking) against one step per pass and the oracle
+# every way the engine can run a single-diffusion program: one step per pass, the
+# two-step pair kernel, and the K-step overlapped-strip kernel at each K / row block /
+# block order
+FUSE_ENVS = [{"MM_FUSE": 0}, {"MM_PASSK": 0}, {"MM_PASSK": 0, "MM_ROWS_PER_WAVE2": 8}, {}] + [
+    {"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th} for k in (1, 2, 3, 4) for th in (16, 32)
+] + [{"MM_XCD_REMAP": 0}]
+
+
+def env_id(env):
+    return ",".join(f"{k[3:]}={v}" for k, v in env.items()) or "default"
+
+
+@pytest.mark.parametrize("env", FUSE_ENVS, ids=env_id)
+@pytest.mark.parametrize("shape", [(1, 1), (2, 3), (3, 5), (5, 2), (37, 53), (130, 257),
+                                   (257, 300), (64, 1000), (9, 124), (70, 125), (33, 241),
+                                   (100, 488)])
+def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
+    # K steps per pass (temporal blocking) against the oracle's single steps; step counts
+    # that are not multiples of K end with a shorter pass
     H, W = shape
-    got = []
-    for env in ({"MM_FUSE": 0}, {}, {"MM_ROWS_PER_WAVE": 16}):
-        e = make_env_engine(gpu, monkeypatch, H, W, **env)
-        e.fill_random(0)
-        e.add_diffuse(0, 0.3)
+    v0 = O.fill_random(H, W)
+    want = {}
+    ref = v0
+    for k in range(1, 10):
+        ref = O.field_step(ref, 0.3)
+        want[k] = ref
+    e = make_env_engine(gpu, monkeypatch, H, W, **env)
+    e.fill_random(0)
+    e.add_diffuse(0, 0.3)
+    done = 0
+    for steps in (1, 3, 5):  # 1, 4, 9 steps in total
         e.run(steps)
-        got.append(e.download())
-        e.close()
-    want = O.field_step(O.fill_random(H, W), 0.3, steps=steps)
-    for g in got:
-        assert np.array_equal(g, want)
+        done += steps
+        assert np.array_equal(e.download(), want[done]), (env, shape, done)
+    e.close()
 
 
-@pytest.mark.parametrize("reduce_every", [1, 2, 3, 4])
-def test_fused_pairs_step_sums(gpu, O, reduce_every):
+@pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 3}, {"MM_STEPS_PER_PASS": 2},
+                                 {"MM_PASSK": 0}], ids=env_id)
+@pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
+def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
     H, W, steps = 130, 257, 12
     v = O.fill_random(H, W)
-    with gpu.Engine(H, W) as e:
-        e.upload(v)
-        e.add_diffuse(0, RATE)
-        e.run(steps, reduce_every)
-        hist = e.sums_history()
-        got = e.download()
+    e = make_env_engine(gpu, monkeypatch, H, W, **env)
+    e.upload(v)
+    e.add_diffuse(0, RATE)
+    e.run(steps, reduce_every)
+    hist = e.sums_history()
+    got = e.download()
+    e.close()
     want = []
     ref = v
     for k in range(1, steps + 1):
@@ -205,6 +227,30 @@ def test_fused_pairs_step_sums(gpu, O, reduce_every):
     assert np.array_equal(got, ref)
     assert hist.shape == (len(want), 1)
     for a, b in zip(hist[:, 0], want):
+        assert abs(a - b) <= 1e-12 * b
+
+
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k):
+    # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
+    # multiple of the graph length, so the tail runs eagerly
+    H, W, steps = 300, 700, 50
+    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k)
+    e.fill_random(0)
+    e.add_diffuse(0, 0.2)
+    e.run(steps, 3)
+    got = e.download()
+    hist = e.sums_history()
+    e.close()
+    ref = O.fill_random(H, W)
+    sums = []
+    for s in range(1, steps + 1):
+        ref = O.field_step(ref, 0.2)
+        if s % 3 == 0:
+            sums.append(math.fsum(ref.ravel()))
+    assert np.array_equal(got, ref)
+    assert hist.shape == (len(sums), 1)
+    for a, b in zip(hist[:, 0], sums):
         assert abs(a - b) <= 1e-12 * b
 
 
@@ -291,27 +337,30 @@ def test_engine_rejects_bad_shapes(gpu):
             e.point_apply(8, 0, 1.0, 0.1)
 
 
-@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
 @pytest.mark.parametrize("graph", [0, 1])
-def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, fuse, graph):
+def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     # The RCCL halo path on one GPU: one rank whose two neighbours are itself
     # (MM_SELF_HALO). Border rows go through ncclSend/ncclRecv on the comm stream, the
     # interior rows run meanwhile, the border rows after the event join -- eagerly and
     # captured in a hipGraph. The received rows land in ghost rows outside the grid, so
-    # the cells must still match the oracle bit for bit.
+    # the cells must still match the oracle bit for bit. k = 1 runs the one-step
+    # kernel; k >= 2 the K-step kernel with a k-row halo every k steps.
     H, W = 64, 300
-    depth = 2 if fuse else 1
+    depth = k
     steps = 2 * depth  # two passes: afterwards the current buffer's ghost rows hold the
                        # rows exchanged in the first pass (the initial state's)
-    for k, v in {"MM_SELF_HALO": 1, "MM_FUSE": fuse, "MM_GRAPH": graph}.items():
-        monkeypatch.setenv(k, str(v))
+    env = {"MM_SELF_HALO": 1, "MM_GRAPH": graph}
+    env.update({"MM_FUSE": 0} if k == 1 else {"MM_STEPS_PER_PASS": k})
+    for key, v in env.items():
+        monkeypatch.setenv(key, str(v))
     e = gpu.Engine(H, W, halo_mode=gpu.MM_HALO_RCCL, comm_id_bytes=gpu.comm_id())
-    for k in ("MM_SELF_HALO", "MM_FUSE", "MM_GRAPH"):
-        monkeypatch.delenv(k)
+    for key in env:
+        monkeypatch.delenv(key)
     v0 = O.fill_random(H, W)
     e.fill_random(0)
     e.add_diffuse(0, RATE)
-    assert e.info()["steps_per_launch"] == (2 if fuse else 1)
+    assert e.info()["steps_per_launch"] == k
     e.run(steps, reduce_every=1)
     got = e.download()
     top = e.read_rows(-depth, depth)

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Tuning sweep of the step kernel (rows per wave x kernel variant) in ONE process,
-interleaved rounds (cdna_hip_programming.md 5.4 rule 24). Prints one JSON line per
-configuration with the median kernel time over rounds. Each variant's result is
-also checked bit-exact against variant 0 on the same input."""
+"""Tuning sweep of the single-attribute step kernels in ONE process, interleaved rounds
+(cdna_hip_programming.md 5.4 rule 24). Each configuration is a set of engine environment
+variables (MM_FUSE, MM_PASSK, MM_STEPS_PER_PASS, MM_ROWS_PER_WAVE[_K|2],
+MM_KERNEL_VARIANT, MM_XCD_REMAP). Prints one JSON line per configuration with the
+median kernel time per launch (HIP events) and the GCUPS it implies, fastest first.
+Every configuration's result is checked bit-exact against the first one."""
 import argparse
 import json
 import os
@@ -15,12 +17,34 @@ import numpy as np  # noqa: E402
 
 import mpimodel as mm  # noqa: E402
 
+ENV_KEYS = ("MM_FUSE", "MM_PASSK", "MM_STEPS_PER_PASS", "MM_ROWS_PER_WAVE",
+            "MM_ROWS_PER_WAVE_K", "MM_ROWS_PER_WAVE2", "MM_KERNEL_VARIANT", "MM_XCD_REMAP")
 
-def make(H, W, th, variant, fuse):
-    os.environ["MM_ROWS_PER_WAVE"] = str(th)
-    os.environ["MM_KERNEL_VARIANT"] = str(variant)
-    os.environ["MM_FUSE"] = str(fuse)
-    e = mm.Engine(H, W)
+PRESETS = {
+    # K-step kernel: K x rows per wave x non-temporal stores x XCD order, plus the
+    # older kernels for comparison
+    "k": [{"MM_FUSE": 0}, {"MM_PASSK": 0}]
+         + [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th, "MM_KERNEL_VARIANT": nt,
+             "MM_XCD_REMAP": x}
+            for k in (2, 3, 4) for th in (16, 32) for nt in (0, 1) for x in (0, 1)],
+    # skewed (variant 0/1) vs unskewed (4/5) level schedule
+    "skew": [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th, "MM_KERNEL_VARIANT": v,
+              "MM_XCD_REMAP": x}
+             for k in (3, 4) for th in (16, 32) for v in (0, 1, 4, 5) for x in (0, 1)],
+    "k-small": [{"MM_PASSK": 0}] + [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th}
+                                    for k in (1, 2, 3, 4) for th in (16, 32)],
+}
+
+
+def make(H, W, env):
+    saved = {k: os.environ.pop(k) for k in ENV_KEYS if k in os.environ}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        e = mm.Engine(H, W)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+        os.environ.update(saved)
     e.fill_random(0)
     e.add_diffuse(0, 0.1)
     return e
@@ -37,45 +61,42 @@ def time_engine(e, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
-    ap.add_argument("--ths", default="8,16,32")
-    ap.add_argument("--variants", default="0,1,3")
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--rows", type=int, default=0, help="rows (default: --size)")
+    ap.add_argument("--preset", default="k", choices=sorted(PRESETS))
+    ap.add_argument("--configs", default="", help="JSON list of env dicts (overrides --preset)")
+    ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--fuse", default="0,1")
     a = ap.parse_args()
-    H = W = a.size
-    ths = [int(x) for x in a.ths.split(",")]
-    vs = [int(x) for x in a.variants.split(",")]
-    fs = [int(x) for x in a.fuse.split(",")]
+    H = a.rows or a.size
+    W = a.size
+    cfgs = json.loads(a.configs) if a.configs else PRESETS[a.preset]
     ref = None
     res = {}
     for rnd in range(a.rounds):
-        for f in fs:
-            for th in ths:
-                if f and th == 32:
-                    continue
-                for v in vs:
-                    if f and v == 3:
-                        continue
-                    e = make(H, W, th, v, f)
-                    e.run(10)
-                    t, b = time_engine(e, a.steps)
-                    per = e.info()["steps_per_launch"]
-                    res.setdefault((f, th, v, per), []).append(t)
-                    if rnd == 0:
-                        out = e.download()
-                        if ref is None:
-                            ref = out
-                        elif not np.array_equal(out, ref):
-                            print(json.dumps({"MISMATCH": [f, th, v]}), flush=True)
-                    e.close()
-    for (f, th, v, per), ts in sorted(res.items(), key=lambda kv: statistics.median(kv[1]) / kv[0][3]):
-        med = statistics.median(ts)
-        print(json.dumps({"size": H, "fuse": f, "th": th, "variant": v,
-                          "us_per_step": round(med * 1e3 / per, 2),
-                          "GCUPS": round(H * W * per / (med * 1e-3) / 1e9, 1),
-                          "kernel_us_med": round(med * 1e3, 2),
-                          "GBps_per_launch": round(16.0 * H * W / (med * 1e-3) / 1e9, 1)}), flush=True)
+        for ci, env in enumerate(cfgs):
+            e = make(H, W, env)
+            e.run(8)
+            t, _ = time_engine(e, a.steps)
+            per = e.info()["steps_per_launch"]
+            res.setdefault(ci, []).append((t, per))
+            if rnd == 0:
+                out = e.download()
+                if ref is None:
+                    ref = out
+                elif not np.array_equal(out, ref):
+                    print(json.dumps({"MISMATCH": env}), flush=True)
+            e.close()
+    rows = []
+    for ci, ts in res.items():
+        med = statistics.median(t for t, _ in ts)
+        per = ts[0][1]
+        rows.append((med / per, {"H": H, "W": W, "env": cfgs[ci], "steps_per_launch": per,
+                                 "kernel_us_med": round(med * 1e3, 2),
+                                 "us_per_step": round(med * 1e3 / per, 2),
+                                 "GCUPS": round(H * W * per / (med * 1e-3) / 1e9, 1),
+                                 "GBps_per_launch": round(16.0 * H * W / (med * 1e-3) / 1e9, 1)}))
+    for _, r in sorted(rows, key=lambda t: t[0]):
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
