@@ -97,10 +97,14 @@ struct mm_engine {
 
     int th = 8;       // rows per wave, one-step kernel
     int th2 = 16;     // rows per wave, fused two-step kernel (MM_PASSK=0)
-    bool passk = true;  // K-step overlapped-strip kernel (mm_passk_kernel) for fusable programs
-    int kpass = 4;      // steps per pass of mm_passk_kernel (MM_STEPS_PER_PASS, 1..4)
-    int thk = 32;       // rows per wave of mm_passk_kernel (MM_ROWS_PER_WAVE_K: 16 / 32)
-    int xcd = 1;        // XCD-contiguous block order for mm_passk_kernel (MM_XCD_REMAP)
+    bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: older kernels)
+    int kpass = 4;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..4)
+    int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
+    double seg_waves = 2.0;  // segment waves per resident wave slot (MM_SEG_WAVES)
+    double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
+    int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
+    int ncu = 0;             // compute units of the device
+    int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -224,7 +228,8 @@ hipEvent_t next_event(mm_engine* e) {
 
 // Launch a pass (fused == 0), a fused two-step pass (fused == 1, `red` = its RED mode)
 // or, with kpass > 0, a K-step pass (mm_passk_kernel, red != 0: per-level sums) covering
-// `rows` rows, with an event pair around it when timing.
+// `rows` rows, with an event pair around it when timing. Algorithmic bytes: every cell of
+// those rows read once and written once per attribute the launch carries.
 int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long long rows,
                  bool time_it, int kpass = 0) {
     hipEvent_t a = nullptr, b = nullptr;
@@ -233,11 +238,11 @@ int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long 
         b = next_event(e);
         if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
         e->ev_bytes.resize(e->ev_used / 2);
-        e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * (fused ? 1 : e->na);
+        e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * ((fused && kpass == 0) ? 1 : e->na);
         MM_HIP(hipEventRecord(a, e->s_comp));
     }
     if (kpass > 0)
-        MM_HIP(mm::launch_passk(kpass, red != 0, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_passk(kpass, e->na, red != 0, A, e->s_comp, e->variant));
     else if (fused)
         MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
     else
@@ -373,16 +378,51 @@ int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it)
     return MM_OK;
 }
 
-// k (1..4) fused steps in one mm_passk_kernel pass; bit j of `mask`: append the sum after
-// step j+1 of the pass to the history. Same two-stream structure as enqueue_pass, with a
-// k-row halo (every k steps) and 4-row blocks for the border launch.
+// Waves of a segment-scheduled range of n rows over ns strips (mm_kernels_k.hip seg_map).
+long long seg_wave_count(long long n, long long ns, long long r, long long re) {
+    if (n <= 0) return 0;
+    if (ns < 3) return ns * ((n + re - 1) / re);
+    return 2 * ((n + re - 1) / re) + (ns - 2) * ((n + r - 1) / r);
+}
+
+// Segment plan of rows [lo, hi) of a k-step pass: r rows per interior-strip segment, re
+// per edge-strip segment (seg_edge x r: the edge strips run the slower general body),
+// the smallest r for which every wave fits seg_waves x the chip's resident wave slots
+// (the kernel's occupancy x CUs), so one launch is one wave generation.
+void seg_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
+    const int nt = e->variant & 1;
+    int& wpc = e->wpc[red ? 1 : 0][nt][e->na][k];
+    if (!wpc) wpc = std::max(1, mm::passk_waves_per_cu(k, e->na, red, nt));
+    const long long want = std::max<long long>(1, (long long)(e->seg_waves * e->ncu * wpc));
+    const long long n = hi - lo, ns = A.nstrips;
+    const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
+    const double units = ns < 3 ? (double)ns / e->seg_edge : (double)(ns - 2) + 2.0 / e->seg_edge;
+    long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
+    r = std::min(std::max<long long>(r, 16), maxr);
+    auto re_of = [&](long long rr) {
+        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * e->seg_edge)));
+    };
+    while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
+    r = std::min(r, maxr);
+    A.seg = 1;
+    A.th = (int)r;
+    A.th_edge = (int)re_of(r);
+    A.ra0 = (int)lo;
+    A.ra1 = (int)hi;
+    A.rb0 = A.rb1 = 0;
+    A.waves_a = A.waves_total = seg_wave_count(n, ns, r, A.th_edge);
+}
+
+// k fused steps of the one-pass program in one mm_passk_kernel pass; bit j of `mask`:
+// append the sums after step j+1 of the pass to the history. Same two-stream structure as
+// enqueue_pass, with a k-row halo (every k steps): the interior rows run as segments
+// beside the exchange, the border rows as 4-row blocks after it.
 int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
     const long long h = e->d.h;
     const int depth = k;
     const bool red = mask != 0;
     mm::PassArgs A;
     fill_args(e, e->passes[0], A);
-    A.th = e->thk;
     A.nstrips = (int)nstrips_k(e, k);
     A.xcd_remap = e->xcd;
     long long total_waves = 0;
@@ -396,14 +436,15 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
         MM_TRY(halo_rccl(e, depth));
         MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
         MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
-        set_ranges(e, A, depth, h - depth, 0, 0);
+        seg_range(e, k, red, A, depth, h - depth);
         const long long interior_waves = A.waves_total;
         mm::PassArgs B = A;
+        B.seg = 0;
         B.th = 4;  // border: short row blocks, the launch is latency-bound
         B.xcd_remap = 0;
         set_ranges(e, B, 0, depth, h - depth, h);
         B.partial_base = interior_waves;
-        MM_HIP(mm::launch_passk(k, red, B, e->s_comm, 0));
+        MM_HIP(mm::launch_passk(k, e->na, red, B, e->s_comm, 0));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
@@ -415,14 +456,14 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
             MM_TRY(begin_halo(e, depth));
             MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
         }
-        set_ranges(e, A, 0, h, 0, 0);
+        seg_range(e, k, red, A, 0, h);
         A.partial_base = 0;
         MM_TRY(launch_timed(e, true, red, A, h, time_it, k));
         total_waves = A.waves_total;
     }
     if (red)
-        MM_HIP(mm::launch_finalize_levels(e->partials, total_waves, k, mask, e->hist, e->hist_n,
-                                          e->hist_cap, e->s_comp));
+        MM_HIP(mm::launch_finalize_levels(e->partials, total_waves, k, e->na, mask, e->hist,
+                                          e->hist_n, e->hist_cap, e->s_comp));
     e->cur ^= 1;
     return MM_OK;
 }
@@ -453,11 +494,27 @@ bool fusable(const mm_engine* e) {
     return e->th2 == 8 || e->th2 == 16;
 }
 
-// Steps one kernel pass advances: kpass with the K-step kernel, 2 with the fused pair
+// Can the program run on mm_passk_kernel? One pass per step (one attribute: a single
+// diffusion; several: diffusions and transfer chains), RCCL or no halo, buffer offsets
+// below 2^31.
+bool passk_ok(const mm_engine* e) {
+    if (!e->fuse_ok || !e->passk || e->passes.size() != 1) return false;
+    if (e->d.nranks > 1 && e->d.halo_mode != MM_HALO_RCCL) return false;
+    if (mm::passk_max_rows(mm::kMaxSteps, e->pitch) < 64) return false;
+    const Pass& p = e->passes[0];
+    if (e->na == 1) return p.diffuse_mask == 1 && p.pre.empty() && p.post.empty();
+    return true;
+}
+
+int passk_steps(const mm_engine* e) {
+    return e->na == 1 ? e->kpass : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
+}
+
+// Steps one kernel pass advances: K with the K-step kernel, 2 with the older fused pair
 // kernel, 1 otherwise.
 int steps_per_launch(const mm_engine* e) {
-    if (!fusable(e)) return 1;
-    return e->passk ? e->kpass : 2;
+    if (passk_ok(e)) return passk_steps(e);
+    return fusable(e) ? 2 : 1;
 }
 
 // Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
@@ -467,9 +524,10 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
     long long s = first;
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
-    if (fuse && e->passk) {
+    if (passk_ok(e)) {
+        const int kp = passk_steps(e);
         while (s < end) {
-            const int k = (int)std::min<long long>(e->kpass, end - s);
+            const int k = (int)std::min<long long>(kp, end - s);
             int mask = 0;
             for (int j = 0; j < k; ++j)
                 if (red(s + j)) mask |= 1 << j;
@@ -548,15 +606,16 @@ int choose_th(const mm_engine* e) {
 }
 
 int ensure_partials(mm_engine* e) {
-    long long need = waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16;
-    // mm_passk_kernel: at most ceil(W/120) strips x (h/16 + 2 border blocks) waves, and
-    // kMaxSteps (= kMaxAttr) partials per wave
-    need = std::max(need, waves_for(nstrips_k(e, mm::kMaxSteps), e->d.h, 16) +
-                              2 * nstrips_k(e, mm::kMaxSteps) + 16);
+    // doubles: older kernels, 128-column strips x 8-row blocks with kMaxAttr sums per wave;
+    // mm_passk_kernel, segments of >= 8 rows (edge strips) plus 4-row border blocks with
+    // K x NA <= 8 sums per wave
+    long long need = (waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16) * mm::kMaxAttr;
+    const long long ns = nstrips_k(e, mm::kMaxSteps);
+    need = std::max(need, (ns * ((e->d.h + 7) / 8 + 4) + 16) * 8);
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
-    MM_HIP(hipMalloc(&e->partials, sizeof(double) * (size_t)need * mm::kMaxAttr));
+    MM_HIP(hipMalloc(&e->partials, sizeof(double) * (size_t)need));
     e->partials_cap = need;
     return MM_OK;
 }
@@ -666,10 +725,15 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
         if (v >= 1 && v <= mm::kMaxSteps) e->kpass = v;
+        if (v >= 1) e->kpass_multi = std::min(v, 2);
     }
-    if (const char* t = std::getenv("MM_ROWS_PER_WAVE_K")) {
-        const int v = std::atoi(t);
-        if (v == 16 || v == 32) e->thk = v;
+    if (const char* f = std::getenv("MM_SEG_WAVES")) {
+        const double v = std::atof(f);
+        if (v > 0.0) e->seg_waves = v;
+    }
+    if (const char* f = std::getenv("MM_SEG_EDGE")) {
+        const double v = std::atof(f);
+        if (v > 0.0 && v <= 1.0) e->seg_edge = v;
     }
     if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
@@ -683,6 +747,8 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     };
     hipError_t he = hipSetDevice(d.device);
     if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
+    he = hipDeviceGetAttribute(&e->ncu, hipDeviceAttributeMultiprocessorCount, d.device);
+    if (he != hipSuccess || e->ncu <= 0) e->ncu = 256;
 
     const size_t per = (size_t)e->rows_alloc * (size_t)e->pitch;  // doubles per buffer
     const size_t per_al = (per + 31) / 32 * 32;                   // 256-B aligned buffers
@@ -770,9 +836,17 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->bytes_device = (long long)e->bytes;
     info->n_passes = (int)e->passes.size();
     const int spl = steps_per_launch(e);
-    const bool k = fusable(e) && e->passk;
-    info->rows_per_wave = k ? e->thk : (fusable(e) ? e->th2 : e->th);
-    info->waves_per_pass = k ? waves_for(nstrips_k(e, spl), e->d.h, e->thk) : waves_for(e, e->d.h);
+    if (passk_ok(e)) {  // the whole-slab segment plan of one pass
+        mm::PassArgs A;
+        std::memset(&A, 0, sizeof A);
+        A.nstrips = (int)nstrips_k(e, spl);
+        seg_range(e, spl, false, A, 0, e->d.h);
+        info->rows_per_wave = A.th;
+        info->waves_per_pass = A.waves_total;
+    } else {
+        info->rows_per_wave = fusable(e) ? e->th2 : e->th;
+        info->waves_per_pass = waves_for(e, e->d.h);
+    }
     info->steps_done = e->steps_done;
     info->fused_attrs = e->na;
     info->steps_per_launch = spl;
@@ -873,9 +947,8 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     }
     // Replay a graph of `per` steps: a whole number of fused pairs, an even number of
     // buffer flips (so the captured pointers are valid again) and of reduction periods.
-    const bool fuse = fusable(e);
     const long long unit = steps_per_launch(e);
-    const long long flips = fuse ? 1 : np;
+    const long long flips = (passk_ok(e) || fusable(e)) ? 1 : np;
     long long len = unit * ((flips % 2) ? 2 : 1);
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
     if (len > 256 || nsteps < len || !e->graphs_ok) {

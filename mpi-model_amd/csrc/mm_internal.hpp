@@ -39,6 +39,8 @@ struct PassArgs {
     double* partials;       // REDUCE: [partial_base + wave][NA] (mm_passk_kernel: [..][K])
     long long partial_base;
     int xcd_remap;          // mm_passk_kernel: XCD-contiguous block order (grid padded to 8)
+    int seg;                // mm_passk_kernel: segment schedule (th / th_edge rows per wave)
+    int th_edge;            // mm_passk_kernel segments: rows per wave of the two edge strips
 };
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
@@ -46,14 +48,21 @@ hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, in
 // Two fused steps of a single-attribute, single-diffusion program (mm_pass2_kernel).
 // red: 0 no sums, 1 second step's sums (partials[wave]), 2 both (partials[wave][2]).
 hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant);
-// K (1..4) fused steps of a single-attribute, single-diffusion program on overlapped
-// strips (mm_passk_kernel, mm_kernels_k.hip); a.th in {4, 16, 32}, a.nstrips =
-// ceil(W / passk_out_cols(k)). red: every level's sums into partials[wave][k].
-hipError_t launch_passk(int k, bool red, const PassArgs& a, hipStream_t s, int variant);
+// K fused steps of a one-pass flow program (NA = 1: K 1..4, one diffusion; NA 2..4:
+// K 1..2, diffusions and transfer chains) on overlapped strips (mm_passk_kernel,
+// mm_kernels_k.hip). a.seg: segment schedule, a.th / a.th_edge rows per wave; else 4-row
+// blocks (a.th = 4). a.nstrips = ceil(W / passk_out_cols(k)). red: every level's sums into
+// partials[wave][k][na]. variant bit 0: non-temporal stores.
+hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t s, int variant);
 int passk_out_cols(int k);
-// Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k],
-// each summed in a fixed order, to the history.
-hipError_t launch_finalize_levels(const double* partials, long long n, int k, int mask,
+int passk_max_steps(int na);
+// largest segment (rows) whose buffer offsets stay below 2^31 at this pitch
+long long passk_max_rows(int k, long long pitch);
+// resident waves per CU of the segment kernel (occupancy API), 0 if unknown
+int passk_waves_per_cu(int k, int na, bool red, int nt);
+// Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k][na],
+// each summed in a fixed order, to the history (na sums per entry).
+hipError_t launch_finalize_levels(const double* partials, long long n, int k, int na, int mask,
                                   double* hist, unsigned long long* hist_n, long long cap,
                                   hipStream_t s);
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,

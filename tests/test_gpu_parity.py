@@ -159,10 +159,10 @@ def test_timed_eager_path_equals_graph_path(gpu, O):
         assert np.array_equal(a.download(), O.field_step(O.fill_random(H, W), RATE, steps=20))
 
 
-def make_env_engine(gpu, monkeypatch, H, W, **env):
+def make_env_engine(gpu, monkeypatch, H, W, n_attr=1, **env):
     for k, v in env.items():
         monkeypatch.setenv(k, str(v))
-    e = gpu.Engine(H, W)
+    e = gpu.Engine(H, W, n_attr=n_attr)
     for k in env:
         monkeypatch.delenv(k)
     return e
@@ -172,8 +172,9 @@ def make_env_engine(gpu, monkeypatch, H, W, **env):
 # two-step pair kernel, and the K-step overlapped-strip kernel at each K / row block /
 # block order
 FUSE_ENVS = [{"MM_FUSE": 0}, {"MM_PASSK": 0}, {"MM_PASSK": 0, "MM_ROWS_PER_WAVE2": 8}, {}] + [
-    {"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th} for k in (1, 2, 3, 4) for th in (16, 32)
-] + [{"MM_XCD_REMAP": 0}]
+    {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3)
+] + [{"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0},
+     {"MM_XCD_REMAP": 1}, {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16}]
 
 
 def env_id(env):
@@ -266,23 +267,29 @@ def add_flows(e, flows):
             e.add_transfer(a, b, r)
 
 
+@pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 1}, {"MM_PASSK": 0},
+                                 {"MM_SEG_WAVES": 64}], ids=env_id)
 @pytest.mark.parametrize("flows,n_attr", [
     (C5_FLOWS, 4),
     ([(1, 0, 0, 0.1), (2, 0, 1, 0.2), (1, 1, 1, 0.3)], 2),       # post-chain, then a 2nd pass
     ([(2, 0, -1, 0.01), (1, 0, 0, 0.1), (1, 0, 0, 0.2)], 1),      # sink, two diffusions of a
-    ([(2, 2, 0, 0.5), (1, 1, 1, 0.1), (2, 1, 2, 0.1)], 3),
+    ([(2, 2, 0, 0.5), (1, 1, 1, 0.1), (2, 1, 2, 0.1)], 3),        # pre + post chain, one pass
+    ([(1, 0, 0, 0.2), (1, 1, 1, 0.3)], 2),                        # two diffusions, one pass
 ])
-def test_flow_program_bit_exact(gpu, O, flows, n_attr):
-    H, W, steps = 67, 300, 4
+@pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9)])
+def test_flow_program_bit_exact(gpu, O, monkeypatch, env, flows, n_attr, shape):
+    H, W = shape
+    steps = 5
     fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(n_attr)]
     want, sums = O.program_step(fields, flows, steps=steps, sums_per_step=True)
-    with gpu.Engine(H, W, n_attr=n_attr) as e:
-        for a in range(n_attr):
-            e.fill_random(a, seed=O.SEED + a)
-        add_flows(e, flows)
-        e.run(steps, reduce_every=1)
-        got = [e.download(a) for a in range(n_attr)]
-        hist = e.sums_history()
+    e = make_env_engine(gpu, monkeypatch, H, W, n_attr=n_attr, **env)
+    for a in range(n_attr):
+        e.fill_random(a, seed=O.SEED + a)
+    add_flows(e, flows)
+    e.run(steps, reduce_every=1)
+    got = [e.download(a) for a in range(n_attr)]
+    hist = e.sums_history()
+    e.close()
     for a in range(n_attr):
         assert np.array_equal(got[a], want[a]), a
     assert hist.shape == (steps, n_attr)

@@ -18,21 +18,18 @@ import numpy as np  # noqa: E402
 import mpimodel as mm  # noqa: E402
 
 ENV_KEYS = ("MM_FUSE", "MM_PASSK", "MM_STEPS_PER_PASS", "MM_ROWS_PER_WAVE",
-            "MM_ROWS_PER_WAVE_K", "MM_ROWS_PER_WAVE2", "MM_KERNEL_VARIANT", "MM_XCD_REMAP")
+            "MM_ROWS_PER_WAVE2", "MM_KERNEL_VARIANT", "MM_XCD_REMAP", "MM_SEG_WAVES",
+            "MM_SEG_EDGE")
 
 PRESETS = {
-    # K-step kernel: K x rows per wave x non-temporal stores x XCD order, plus the
-    # older kernels for comparison
-    "k": [{"MM_FUSE": 0}, {"MM_PASSK": 0}]
-         + [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th, "MM_KERNEL_VARIANT": nt,
-             "MM_XCD_REMAP": x}
-            for k in (2, 3, 4) for th in (16, 32) for nt in (0, 1) for x in (0, 1)],
-    # skewed (variant 0/1) vs unskewed (4/5) level schedule
-    "skew": [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th, "MM_KERNEL_VARIANT": v,
-              "MM_XCD_REMAP": x}
-             for k in (3, 4) for th in (16, 32) for v in (0, 1, 4, 5) for x in (0, 1)],
-    "k-small": [{"MM_PASSK": 0}] + [{"MM_STEPS_PER_PASS": k, "MM_ROWS_PER_WAVE_K": th}
-                                    for k in (1, 2, 3, 4) for th in (16, 32)],
+    # segment-scheduled K-step kernel: K x waves per slot x edge-strip length x
+    # non-temporal stores, plus the older kernels for comparison
+    "seg": [{"MM_FUSE": 0}, {"MM_PASSK": 0}]
+           + [{"MM_STEPS_PER_PASS": k, "MM_SEG_WAVES": f, "MM_KERNEL_VARIANT": nt}
+              for k in (2, 3, 4) for f in (1, 2) for nt in (0, 1)]
+           + [{"MM_STEPS_PER_PASS": 4, "MM_SEG_EDGE": 1.0}, {"MM_STEPS_PER_PASS": 4, "MM_SEG_WAVES": 4},
+              {"MM_STEPS_PER_PASS": 4, "MM_SEG_WAVES": 0.75}, {"MM_STEPS_PER_PASS": 4, "MM_XCD_REMAP": 1}],
+    "k-small": [{"MM_PASSK": 0}] + [{"MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 4)],
 }
 
 
@@ -62,7 +59,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--rows", type=int, default=0, help="rows (default: --size)")
-    ap.add_argument("--preset", default="k", choices=sorted(PRESETS))
+    ap.add_argument("--preset", default="seg", choices=sorted(PRESETS))
     ap.add_argument("--configs", default="", help="JSON list of env dicts (overrides --preset)")
     ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--rounds", type=int, default=3)
@@ -77,8 +74,11 @@ def main():
             e = make(H, W, env)
             e.run(8)
             t, _ = time_engine(e, a.steps)
-            per = e.info()["steps_per_launch"]
+            info = e.info()
+            per = info["steps_per_launch"]
             res.setdefault(ci, []).append((t, per))
+            if rnd == 0:
+                cfgs[ci] = dict(cfgs[ci], _rows=info["rows_per_wave"], _waves=info["waves_per_pass"])
             if rnd == 0:
                 out = e.download()
                 if ref is None:
