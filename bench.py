@@ -11,7 +11,7 @@ workload: default "c2" = BASELINE.json configs[1]: 4096 x 4096 fp64 cells per GP
           chained transfers + 4 diffusions, per-step sums).
 step    : one pass of the flow over the whole grid (all passes of the program).
 timing  : W untimed warmup steps, then exactly K steps on the production path (hipGraph
-          replay of fused step pairs) bracketed by a barrier and a device-wide
+          replay of K-step kernel passes) bracketed by a barrier and a device-wide
           synchronize (hipDeviceSynchronize) on both sides; the max over ranks is reported. Inputs are resident in HBM
           (generated on the device) before timing. Then the same K steps again, launched
           eagerly with a HIP event pair around every step kernel on its own stream: the
@@ -76,12 +76,30 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_ranks():
+    """Host cores for the CPU baseline: MM_CPU_RANKS, else min(16, cpu_count) -- the GPU
+    box gives one GPU's job a 16-CPU share while os.cpu_count() shows the whole machine."""
+    n = int(os.environ.get("MM_CPU_RANKS", "0"))
+    return n if n > 0 else max(1, min(16, os.cpu_count() or 1))
+
+
 def cpu_baseline(H, W, seconds):
-    """The oracle's scalar C port of the same step (oracle/mm_oracle.c), one core, on a
-    bounded sample: as many whole steps of the same grid as fit in `seconds`."""
+    """The reference's CPU decomposition over the oracle's step (oracle/mm_cpu_mpi.c: row
+    slabs, one MPI rank per core, blocking border-row exchange every step) on the same grid
+    and inputs, as many whole steps as fit in about `seconds`. Without an MPI it falls back
+    to the scalar single-core port (oracle/mm_oracle.c or_field_step)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import numpy as np
     import oracle
+    ranks = cpu_ranks()
+    if os.path.exists(os.path.join(oracle.MPI_HOME, "bin", "mpirun")):
+        r = oracle.cpu_mpi(H, W, RATE, seconds, ranks, timeout=max(120, 10 * seconds))
+        return {"value": r["GCUPS"], "unit": "GCUPS", "cores": r["ranks"], "kind": "port",
+                "sample": f"{r['steps']} timed steps (after {r['warmup_steps']} untimed) of the "
+                          f"{H}x{W} fp64 grid, {r['ranks']} MPI ranks x 1 core, row slabs + "
+                          f"blocking border-row MPI_Sendrecv per step (the reference's "
+                          f"decomposition), oracle step (oracle/mm_cpu_mpi.c, -O3), "
+                          f"{r['seconds']:.1f} s"}
+    import numpy as np
     v = oracle.fill_random(H, W)
     o = np.empty_like(v)
     L = oracle.lib()
@@ -97,7 +115,7 @@ def cpu_baseline(H, W, seconds):
             break
     return {"value": H * W * steps / el / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
             "sample": f"{steps} steps of the {H}x{W} fp64 grid, oracle/mm_oracle.c "
-                      f"or_field_step (scalar C, -O2), {el:.1f} s"}
+                      f"or_field_step (scalar C, -O2, no MPI found), {el:.1f} s"}
 
 
 def main():
@@ -190,13 +208,17 @@ def main():
     if rank == 0:
         kern_avg_ms = kern_ms / max(n_launch, 1)
         launches_per_step = n_launch / max(args.steps, 1)
-        fused = info["steps_per_launch"] == 2
+        spl = info["steps_per_launch"]
+        kname = ("mm_pass_kernel", "mm_pass2_kernel", "mm_passk_kernel")[info["kernel"]]
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         traffic = None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):
+        if os.path.exists(tf):  # only when it was measured on this kernel
             with open(tf) as f:
-                traffic = json.load(f).get(f"{args.workload}_n{N}_bytes_per_launch")
+                pmc = json.load(f)
+            if kname in pmc.get(f"{args.workload}_n{N}_kernel", "") and \
+                    pmc.get(f"{args.workload}_n{N}_steps_per_launch", spl) == spl:
+                traffic = pmc.get(f"{args.workload}_n{N}_bytes_per_launch")
         cons = abs(s_after - s_before) / abs(s_before)
         line = {
             "metric": "cell-updates/s (GCUPS) per step + % of HBM roofline",
@@ -213,8 +235,7 @@ def main():
             "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
                     "seed 0x4D50494D, generated on the device",
             "config": {"workload": f"{args.workload}: {wl['desc']}", "grid": [H, W],
-                       "path": "hipGraph replay, " + ("two fused steps per kernel pass"
-                                                      if fused else "one step per pass"),
+                       "path": f"hipGraph replay, {kname}, {spl} fused step(s) per kernel pass",
                        "rows_per_gpu": h, "n_attr": na, "rate": RATE,
                        "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else "")
                        + (" (self-halo: RCCL exchange with itself)" if args.self_halo else ""),
@@ -227,13 +248,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
-                "kernel": "mm_pass2_kernel" if fused else "mm_pass_kernel",
+                "kernel": kname,
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "steps_per_launch": info["steps_per_launch"],
                 "launches_per_step": launches_per_step,
                 # BASELINE.md's formula: GCUPS x 16 B x A / 8 TB/s (per GPU); above 1.0
-                # when two steps share one HBM round trip (temporal blocking)
+                # when K steps share one HBM round trip (temporal blocking)
                 "equivalent_frac": round(gcups / N * 16.0 * na / HBM_PEAK_GBS, 4),
             },
             "check": {"total_rel_drift": cons},

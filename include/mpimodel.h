@@ -86,7 +86,8 @@ typedef struct mm_info {
     long long waves_per_pass;  /* waves launched per pass */
     long long steps_done;      /* steps run since the last fill/upload */
     int fused_attrs;           /* attributes carried per fused pass */
-    int steps_per_launch;      /* 2: the program runs as fused step pairs (temporal blocking) */
+    int steps_per_launch;      /* steps fused per kernel pass (temporal blocking), 1..4 */
+    int kernel;                /* step kernel: 0 mm_pass_kernel, 1 mm_pass2_kernel, 2 mm_passk_kernel */
 } mm_info;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

@@ -843,7 +843,9 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         seg_range(e, spl, false, A, 0, e->d.h);
         info->rows_per_wave = A.th;
         info->waves_per_pass = A.waves_total;
+        info->kernel = 2;
     } else {
+        info->kernel = spl == 2 ? 1 : 0;
         info->rows_per_wave = fusable(e) ? e->th2 : e->th;
         info->waves_per_pass = waves_for(e, e->d.h);
     }

@@ -1,612 +1,10 @@
-// mm_kernels_k.hip -- K fused flow-program steps per HBM pass (temporal blocking), gfx950.
-//
-// The hot path: the generalisation of src/Model.hpp:176-235 +
-// src/Exponencial.hpp:18-20 to every cell and every step -- one whole-grid Exponencial
-// flow per attribute, with optional same-cell transfer chains before / after it (config
-// C5). A pass reads every cell once, advances it K steps in registers and writes it once,
-// so HBM moves 16/K B per cell-update and attribute instead of 16 B.
-//
-// Overlapped strips. A wave owns a strip of 128 LOADED columns (lane l: columns
-// c0+2l, c0+2l+1 as one 16-B buffer load per attribute) but outputs only the inner
-// 128-4L columns, L = ceil(K/2) lanes on each side. Every level of the K-step pipeline
-// computes all 64 lanes with exactly the same instructions; the y+-1 neighbours come from
-// the adjacent lanes through DPP wave_shr:1 / wave_shl:1, and the lanes at the wave's
-// edges receive garbage that moves one column inward per level -- after K levels it has
-// reached columns < K from each edge, i.e. the L halo lanes, whose results are
-// discarded. No edge-column loads, no per-lane special cases; the price is 4L/128 extra
-// (L2-resident) column reads.
-//
-// Rows. The wave slides down its strip, input rows rA-K .. rB+K-1 one by one (U rows
-// prefetched). Level j (1..K) keeps a three-row window per attribute in registers
-// (shares of the row above; shares and u - out of the current row) and emits one row
-// per input row. The levels are SKEWED: at iteration i level j consumes the row level
-// j-1 emitted at iteration i-1, so the K levels of one iteration are independent
-// instruction streams that interleave (instead of one K-deep dependent chain per input
-// row). Level j's m-th input is row rA-K+(j-1)+m, at iteration m + 3(j-1); it emits row
-// rA-K-2j+1+i. Level K's rows rA..rB-1 are stored; lower levels compute K-j rows beyond
-// the segment on each side (recomputed by the neighbouring segment).
-//
-// Two schedules of that pipeline:
-//   * SEGMENT (interior and whole-slab passes): a wave runs a tall segment of rows (row
-//     counts at run time, sized so the chip's wave slots hold every wave at once). A
-//     compile-time prologue fills the levels, then a runtime loop streams the segment with
-//     all K levels active: the row overhead of temporal blocking is K(K-1) level-rows per
-//     segment. The two edge strips (their first / last grid column has 5 or 3
-//     neighbours: true divisions, the slow body) get shorter segments and are dispatched
-//     first, so the waves of a launch finish together;
-//   * BLOCK: 4 rows, fully unrolled -- the border rows of a halo-split pass.
-//
-// Every level uses exactly the single-step arithmetic of oracle/mm_oracle.h (transfers
-// in declared order, then out = r*u, s = out/cnt, v' = (u - out) + nb), so K fused steps
-// are bit-identical to K single steps (built with -ffp-contract=off).
-#include "mm_internal.hpp"
+// mm_kernels_k.hip -- dispatch of the K-step kernel (templates: mm_passk.hpp, instances:
+// mm_passk_k1..4.hip) and the fixed-order level-sum finalize kernel.
+#include "mm_passk.hpp"
 
 namespace mm {
 
 namespace {
-
-typedef double dv2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr unsigned kOOBk = 0x80000000u;  // voffset past any num_records: load 0 / drop store
-constexpr int kSeg = 0;                  // MODE value of the segment schedule
-
-// input rows prefetched per wave: 8 KiB in flight for one attribute, ~8 KiB for more
-template <int NA>
-constexpr int seg_prefetch() {
-    return NA == 1 ? 8 : (NA == 2 ? 4 : 2);
-}
-
-// mov_dpp has no tied "old" operand, so the result can land in a fresh register without
-// first copying the source; lanes without a source lane read 0 (bound_ctrl) -- only the
-// halo lanes at the wave's edges, whose results are discarded.
-__device__ __forceinline__ double dpp_lower(double src) {
-    // lane i <- lane i-1 (wave_shr:1)
-    const long long s = __double_as_longlong(src);
-    const int lo = __builtin_amdgcn_mov_dpp((int)s, 0x138, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(s >> 32), 0x138, 0xf, 0xf, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ double dpp_upper(double src) {
-    // lane i <- lane i+1 (wave_shl:1)
-    const long long s = __double_as_longlong(src);
-    const int lo = __builtin_amdgcn_mov_dpp((int)s, 0x130, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(s >> 32), 0x130, 0xf, 0xf, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// 1 + (i > 0) + (i < n-1) inside [0, n), 0 outside: cnt = span(x)*span(y) - 1
-__device__ __forceinline__ int span3k(long long n, long long i) {
-    return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
-}
-
-__device__ __forceinline__ double share_k(double out, int cnt) {
-    return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
-}
-
-// Descriptor of `rows` consecutive rows starting at `first` (pointer already offset):
-// row k of the range is at byte offset k*pitch*8 (added to the lane's voffset), offsets
-// past the range -- later rows, or lanes whose voffset is kOOBk -- load 0 / drop stores.
-// One descriptor per wave and attribute instead of one per row keeps the unrolled rows
-// from holding dozens of scalar descriptors (which spilled SGPRs into VGPR lanes). The
-// engine keeps every offset below 2^31 (passk_max_rows).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double* first, int rows,
-                                                            long long pitch) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(first), 0,
-                                             rows > 0 ? (int)(rows * pitch * 8) : 0, 0x00020000);
-}
-
-__device__ __forceinline__ dv2 load_row(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-template <int NT>
-__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, unsigned off, double w0,
-                                          double w1) {
-    dv2 v;
-    v.x = w0;
-    v.y = w1;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0,
-                                           (NT & 1) ? 2 : 0);
-}
-
-// One level's three-row window of one attribute: shares of the row above (p), shares
-// and u - out of the current row (c).
-struct Win {
-    double sp0, sp1, sc0, sc1, dc0, dc1;
-};
-
-// What every level of one wave needs besides its windows.
-struct Lane {
-    long long H, gx0;  // grid rows, global row of local row 0
-    int sy0, sy1;      // column spans of this lane's two columns
-    bool fast_cols;    // all loaded columns interior
-    bool own0, own1;   // this lane's columns are output cells of this wave
-};
-
-// Transfers of a chain, in declared order, on one cell's attribute values: out = r*u_a;
-// u_a -= out; u_b += out (b < 0: the outflow leaves the system). Chain entries are read
-// with compile-time indices only (scalar loads of the kernel arguments).
-template <int NA>
-__device__ __forceinline__ void chain_k(double (&u)[NA], int n, const signed char* ta,
-                                        const signed char* tb, const double* tr) {
-#pragma unroll
-    for (int t = 0; t < kMaxChain; ++t) {
-        if (t >= n) break;  // wave-uniform
-        const int a = ta[t], b = tb[t];
-        const double r = tr[t];
-        double src = 0.0;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) src = u[k];
-        const double out = r * src;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) u[k] = u[k] - out;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == b) u[k] = u[k] + out;
-    }
-}
-
-// Pre-chain, then per diffusing attribute out = rate*u, s = out/cnt, d = u - out for this
-// lane's two columns of row gx (src/Exponencial.hpp:18-20, src/Model.hpp:199); cells
-// outside the grid emit nothing; attributes that do not diffuse pass through (s = 0).
-template <int NA, bool FAST, bool CHAIN>
-__device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long long gx,
-                                       double (&u0)[NA], double (&u1)[NA], double (&s0)[NA],
-                                       double (&s1)[NA], double (&d0)[NA], double (&d1)[NA]) {
-    if (CHAIN && A.npre) {
-        chain_k<NA>(u0, A.npre, A.pre_a, A.pre_b, A.pre_r);
-        chain_k<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
-    }
-    const int sx = FAST ? 3 : span3k(c.H, gx);
-    const bool inner = FAST || (sx == 3 && c.fast_cols);  // wave-uniform
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-        if (NA > 1 && !((A.diffuse_mask >> a) & 1)) {
-            s0[a] = s1[a] = 0.0;
-            d0[a] = u0[a];
-            d1[a] = u1[a];
-            continue;
-        }
-        const double r = A.drate[a];
-        if (inner) {  // interior row, interior strip: cnt == 8
-            const double o0 = r * u0[a], o1 = r * u1[a];
-            s0[a] = o0 * 0.125;
-            s1[a] = o1 * 0.125;
-            d0[a] = u0[a] - o0;
-            d1[a] = u1[a] - o1;
-        } else if (sx == 0) {  // row outside the grid
-            s0[a] = s1[a] = 0.0;
-            d0[a] = u0[a];
-            d1[a] = u1[a];
-        } else {
-            const int k0 = c.sy0 ? sx * c.sy0 - 1 : 0;
-            const int k1 = c.sy1 ? sx * c.sy1 - 1 : 0;
-            const double o0 = k0 > 0 ? r * u0[a] : 0.0;
-            const double o1 = k1 > 0 ? r * u1[a] : 0.0;
-            s0[a] = share_k(o0, k0);
-            s1[a] = share_k(o1, k1);
-            d0[a] = u0[a] - o0;
-            d1[a] = u1[a] - o1;
-        }
-    }
-}
-
-// Level input row m = 0 or 1 (global row gx): fill the windows.
-template <int NA, bool FAST, bool CHAIN>
-__device__ __forceinline__ void level_fill(const PassArgs& A, const Lane& c, long long gx, int m,
-                                           Win (&w)[NA], double (&u0)[NA], double (&u1)[NA]) {
-    double s0[NA], s1[NA], d0[NA], d1[NA];
-    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, s0, s1, d0, d1);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-        if (m == 0) {
-            w[a].sp0 = s0[a];
-            w[a].sp1 = s1[a];
-        } else {
-            w[a].sc0 = s0[a];
-            w[a].sc1 = s1[a];
-            w[a].dc0 = d0[a];
-            w[a].dc1 = d1[a];
-        }
-    }
-}
-
-// Level input row m >= 2 (global row gx): emit the windows' current row (then the
-// post-chain) and slide the windows.
-// v' = (u - out) + nb, nb = (c3(y-1) + c3(y+1)) + p with p = s(x-1) + s(x+1) and
-// c3 = p + s(x) (src/Model.hpp:206-211,234; the order fixed by oracle/mm_oracle.h).
-template <int NA, bool FAST, bool CHAIN>
-__device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, long long gx,
-                                           Win (&w)[NA], double (&u0)[NA], double (&u1)[NA],
-                                           double (&w0)[NA], double (&w1)[NA]) {
-    double sn0[NA], sn1[NA], dn0[NA], dn1[NA];
-    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, sn0, sn1, dn0, dn1);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-        if (NA > 1 && !((A.diffuse_mask >> a) & 1)) {
-            w0[a] = w[a].dc0;
-            w1[a] = w[a].dc1;
-        } else {
-            const double p0 = w[a].sp0 + sn0[a], p1 = w[a].sp1 + sn1[a];
-            const double c0 = p0 + w[a].sc0, c1 = p1 + w[a].sc1;
-            const double left = dpp_lower(c1);   // c3 at column y0-1 (lane-1's second column)
-            const double right = dpp_upper(c0);  // c3 at column y0+2 (lane+1's first column)
-            w0[a] = w[a].dc0 + ((left + c1) + p0);
-            w1[a] = w[a].dc1 + ((c0 + right) + p1);
-        }
-        w[a].sp0 = w[a].sc0;
-        w[a].sp1 = w[a].sc1;
-        w[a].sc0 = sn0[a];
-        w[a].sc1 = sn1[a];
-        w[a].dc0 = dn0[a];
-        w[a].dc1 = dn1[a];
-    }
-    if (CHAIN && A.npost) {
-        chain_k<NA>(w0, A.npost, A.post_a, A.post_b, A.post_r);
-        chain_k<NA>(w1, A.npost, A.post_a, A.post_b, A.post_r);
-    }
-}
-
-// Add an emitted row's owned cells to a level sum. The empty asm materialises the sum
-// here: otherwise LLVM sinks the whole chain of adds to the kernel exit and keeps every
-// row's values live until then.
-__device__ __forceinline__ void accum(double& acc, bool own, const Lane& c, double w0, double w1) {
-    acc = acc + ((own && c.own0) ? w0 : 0.0);
-    acc = acc + ((own && c.own1) ? w1 : 0.0);
-    asm volatile("" : "+v"(acc));
-}
-
-__device__ __forceinline__ double wave_sum_k(double v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
-    return v;
-}
-
-template <int K, int NA>
-__device__ __forceinline__ void write_sums(const PassArgs& A, long long wid, int lane,
-                                           double (&acc)[K][NA]) {
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            const double t = wave_sum_k(acc[j][a]);
-            if (lane == 0) A.partials[((A.partial_base + wid) * K + j) * NA + a] = t;
-        }
-}
-
-// The per-wave buffers of one pass: NA input and output row ranges.
-template <int K, int NA>
-struct Bufs {
-    __amdgpu_buffer_rsrc_t in[NA], out[NA];
-    __device__ __forceinline__ Bufs(const PassArgs& A, int rA, int rB) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            in[a] = rows_rsrc(A.in[a] + (long long)(rA - K) * A.pitch, rB - rA + 2 * K, A.pitch);
-            out[a] = rows_rsrc(A.out[a] + (long long)rA * A.pitch, rB - rA, A.pitch);
-        }
-    }
-};
-
-// BLOCK schedule: TH rows, every iteration unrolled at compile time (level fill states,
-// row offsets and block ownership are all constants).
-template <int K, int TH, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
-__device__ __forceinline__ void passk_block(const PassArgs& A, const Lane& c, long long wid,
-                                            int lane, int rA, int rB, unsigned voff,
-                                            unsigned soff) {
-    constexpr int NI = TH + 2 * K;       // input rows
-    constexpr int NIT = TH + 3 * K - 1;  // iterations
-    double acc[K][NA];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) acc[j][a] = 0.0;
-    const unsigned rowb = (unsigned)(A.pitch * 8);
-    const Bufs<K, NA> B(A, rA, rB);
-    dv2 raw[U][NA];
-#pragma unroll
-    for (int k = 0; k < U; ++k)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) raw[k][a] = load_row(B.in[a], voff + k * rowb);
-    Win win[K][NA];
-    double pend0[K][NA], pend1[K][NA];  // level j's row of the previous iteration: pend[j-1]
-
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-#pragma unroll
-        for (int j = K; j >= 1; --j) {  // descending: pend[j-2] is read before it is refilled
-            const int m = i - 3 * (j - 1);
-            if (m < 0 || m >= NI - 2 * (j - 1)) continue;  // compile-time
-            double u0[NA], u1[NA];
-#pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                if (j == 1) {
-                    u0[a] = raw[i % U][a].x;
-                    u1[a] = raw[i % U][a].y;
-                    if (i + U < NI) raw[i % U][a] = load_row(B.in[a], voff + (i + U) * rowb);
-                } else {
-                    u0[a] = pend0[j - 2][a];
-                    u1[a] = pend1[j - 2][a];
-                }
-            }
-            const long long gx = c.gx0 + rA - K + (j - 1) + m;
-            if (m < 2) {
-                level_fill<NA, FAST, CHAIN>(A, c, gx, m, win[j - 1], u0, u1);
-                continue;
-            }
-            double w0[NA], w1[NA];
-            level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-            const int orow = m + j - K - 2;  // output row - rA (compile-time)
-#pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                if (RED && orow >= 0 && orow < TH)
-                    accum(acc[j - 1][a], rA + orow < rB, c, w0[a], w1[a]);
-                if (j == K) {
-                    store_row<NT>(B.out[a], soff + orow * rowb, w0[a], w1[a]);
-                } else {
-                    pend0[j - 1][a] = w0[a];
-                    pend1[j - 1][a] = w1[a];
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the row order: bounds the live registers
-    }
-    if (RED) write_sums<K, NA>(A, wid, lane, acc);
-}
-
-// SEGMENT schedule: R = rB - rA rows (run time). Iterations 0 .. 3K-2 fill the levels
-// (compile-time); from iteration I0 = 3K-1 on every level emits, level K writes row
-// rA + (i - I0), and the loop runs R iterations (rounded up to U; the extra ones read
-// zeros past the input rows and their stores fall past the output rows).
-template <int K, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
-__device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, long long wid,
-                                              int lane, int rA, int rB, unsigned voff,
-                                              unsigned soff) {
-    constexpr int I0 = 3 * K - 1;
-    const int R = rB - rA;
-    double acc[K][NA];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) acc[j][a] = 0.0;
-    const unsigned rowb = (unsigned)(A.pitch * 8);
-    const Bufs<K, NA> B(A, rA, rB);
-    dv2 raw[U][NA];
-#pragma unroll
-    for (int k = 0; k < U; ++k)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) raw[k][a] = load_row(B.in[a], voff + k * rowb);
-    Win win[K][NA];
-    double pend0[K][NA], pend1[K][NA];
-
-    // prologue: level j takes part from iteration 3(j-1); nothing is stored yet
-#pragma unroll
-    for (int i = 0; i < I0; ++i) {
-#pragma unroll
-        for (int j = K; j >= 1; --j) {
-            const int m = i - 3 * (j - 1);
-            if (m < 0) continue;  // compile-time
-            double u0[NA], u1[NA];
-#pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                if (j == 1) {
-                    u0[a] = raw[i % U][a].x;
-                    u1[a] = raw[i % U][a].y;
-                    raw[i % U][a] = load_row(B.in[a], voff + (i + U) * rowb);
-                } else {
-                    u0[a] = pend0[j - 2][a];
-                    u1[a] = pend1[j - 2][a];
-                }
-            }
-            const long long gx = c.gx0 + rA - K + (j - 1) + m;
-            if (m < 2) {
-                level_fill<NA, FAST, CHAIN>(A, c, gx, m, win[j - 1], u0, u1);
-                continue;
-            }
-            double w0[NA], w1[NA];
-            level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-            const int r = rA - K - 2 * j + 1 + i;  // output row
-#pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
-                pend0[j - 1][a] = w0[a];  // j < K here: level K's m <= 1 in the prologue
-                pend1[j - 1][a] = w1[a];
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-
-    // steady state: every level emits one row per iteration
-    for (int base = I0; base < I0 + R; base += U) {
-#pragma unroll
-        for (int t = 0; t < U; ++t) {
-            const int i = base + t;
-            const int slot = (I0 + t) % U;  // base = I0 (mod U)
-#pragma unroll
-            for (int j = K; j >= 1; --j) {
-                double u0[NA], u1[NA];
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    if (j == 1) {
-                        u0[a] = raw[slot][a].x;
-                        u1[a] = raw[slot][a].y;
-                        raw[slot][a] = load_row(B.in[a], voff + (unsigned)(i + U) * rowb);
-                    } else {
-                        u0[a] = pend0[j - 2][a];
-                        u1[a] = pend1[j - 2][a];
-                    }
-                }
-                const long long gx = c.gx0 + rA - K + i - 2 * (j - 1);
-                double w0[NA], w1[NA];
-                level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-                const int r = rA - K - 2 * j + 1 + i;  // output row
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
-                    if (j == K) {
-                        store_row<NT>(B.out[a], soff + (unsigned)(i - I0) * rowb, w0[a], w1[a]);
-                    } else {
-                        pend0[j - 1][a] = w0[a];
-                        pend1[j - 1][a] = w1[a];
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    if (RED) write_sums<K, NA>(A, wid, lane, acc);
-}
-
-// Segment wave -> (strip, rows) inside one row range [lo, hi): the two edge strips come
-// first, in segments of re rows; then the other strips in segments of r rows, strips
-// fastest, the top and bottom segments (rows next to the grid's first / last row) first.
-// Slow work is cut shorter and dispatched first, so the waves of a launch end together.
-__device__ __forceinline__ void seg_map(long long w, int lo, int hi, int ns, int r, int re,
-                                        int& strip, int& rA, int& rB) {
-    const int n = hi - lo;
-    int rb, rows;
-    if (ns < 3) {
-        strip = (int)(w % ns);
-        rb = (int)(w / ns);
-        rows = re;
-    } else {
-        const int nbe = (n + re - 1) / re;
-        if (w < 2LL * nbe) {
-            strip = w < nbe ? 0 : ns - 1;
-            rb = (int)(w % nbe);
-            rows = re;
-        } else {
-            const long long t = w - 2LL * nbe;
-            const int nb = (n + r - 1) / r;
-            strip = 1 + (int)(t % (ns - 2));
-            const int q = (int)(t / (ns - 2));
-            rb = q == 0 ? 0 : (q == 1 ? nb - 1 : q - 1);
-            rows = r;
-        }
-    }
-    rA = lo + rb * rows;
-    rB = min(rA + rows, hi);
-}
-
-// K steps of the one-pass flow program per launch, NA attributes, transfer chains when
-// CHAIN. MODE: kSeg = segment schedule (A.th / A.th_edge rows per wave), else the block
-// schedule with MODE rows per wave. U input rows prefetched. RED: per-level sums of the
-// owned cells into partials[((partial_base + wave) * K + level) * NA + attribute].
-// NT & 1: non-temporal stores.
-template <int K, int MODE, int U, bool RED, int NT, int NA, bool CHAIN>
-__global__ __launch_bounds__(kBlock) void mm_passk_kernel(const PassArgs A) {
-    constexpr int L = (K + 1) / 2;          // halo lanes per side
-    constexpr int OC = kStripCols - 4 * L;  // output columns per strip
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // optional XCD-aware block order: hardware block b runs on XCD b % 8; logical block
-    // (b % 8) * per + b / 8 gives every XCD a contiguous run of tiles
-    long long blk = blockIdx.x;
-    if (A.xcd_remap) {
-        const long long per = gridDim.x / 8;
-        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    }
-    const long long wid = blk * kWavesPerBlock + wave;
-    if (wid >= A.waves_total) return;
-
-    int rlo, rhi;
-    long long w = wid;
-    if (w < A.waves_a) {
-        rlo = A.ra0;
-        rhi = A.ra1;
-    } else {
-        w -= A.waves_a;
-        rlo = A.rb0;
-        rhi = A.rb1;
-    }
-    int strip, rA, rB;
-    if (MODE == kSeg) {
-        seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, strip, rA, rB);
-    } else {
-        strip = (int)(w % A.nstrips);
-        rA = rlo + (int)(w / A.nstrips) * MODE;
-        rB = min(rA + MODE, rhi);
-    }
-
-    const long long W = A.W;
-    const long long c0 = (long long)strip * OC - 2 * L;  // first loaded column (even)
-    const long long y0 = c0 + 2 * lane;
-    const bool in_row = y0 >= 0 && y0 < A.pitch;  // y0 even, pitch a multiple of 128
-    const unsigned voff = in_row ? (unsigned)(y0 * 8) : kOOBk;
-    const bool store_lane = lane >= L && lane < 64 - L && y0 < W;
-    // columns past W inside the pitch are padding: writing them is harmless
-    const unsigned soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
-    Lane c;
-    c.H = A.H;
-    c.gx0 = A.x_init;
-    c.sy0 = span3k(W, y0);
-    c.sy1 = span3k(W, y0 + 1);
-    c.fast_cols = c0 >= 1 && c0 + kStripCols <= W - 1;  // loaded cols in [1, W-2]
-    c.own0 = store_lane;
-    c.own1 = store_lane && y0 + 1 < W;
-
-    // a wave whose input rows and loaded columns are all interior (cnt == 8 everywhere)
-    // runs the branch-free body; edge waves run the general one
-    const bool fast = c.fast_cols && c.gx0 + rA - K >= 1 && c.gx0 + rB + K - 1 <= A.H - 2;
-    if constexpr (MODE == kSeg) {
-        if (fast)
-            passk_segment<K, U, RED, NT, true, NA, CHAIN>(A, c, wid, lane, rA, rB, voff, soff);
-        else
-            passk_segment<K, U, RED, NT, false, NA, CHAIN>(A, c, wid, lane, rA, rB, voff, soff);
-    } else {
-        if (fast)
-            passk_block<K, MODE, U, RED, NT, true, NA, CHAIN>(A, c, wid, lane, rA, rB, voff, soff);
-        else
-            passk_block<K, MODE, U, RED, NT, false, NA, CHAIN>(A, c, wid, lane, rA, rB, voff,
-                                                              soff);
-    }
-}
-
-constexpr int kBorderRows = 4;  // block schedule rows (border launches)
-
-template <int K, int MODE, int U, int NT, int NA, bool CHAIN>
-hipError_t launch_k3(bool red, const PassArgs& a, hipStream_t s) {
-    long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (a.xcd_remap) blocks = (blocks + 7) / 8 * 8;
-    const dim3 g((unsigned)blocks), b(kBlock);
-    if (red)
-        hipLaunchKernelGGL((mm_passk_kernel<K, MODE, U, true, NT, NA, CHAIN>), g, b, 0, s, a);
-    else
-        hipLaunchKernelGGL((mm_passk_kernel<K, MODE, U, false, NT, NA, CHAIN>), g, b, 0, s, a);
-    return hipGetLastError();
-}
-
-// a.seg: segment schedule (variant bit 0: non-temporal stores); else 4-row blocks.
-template <int K, int NA, bool CHAIN>
-hipError_t launch_k2(bool red, const PassArgs& a, hipStream_t s, int v) {
-    constexpr int U = seg_prefetch<NA>();
-    if (!a.seg) {
-        if (a.th != kBorderRows) return hipErrorInvalidValue;
-        return launch_k3<K, kBorderRows, (U < 4 ? U : 4), 0, NA, CHAIN>(red, a, s);
-    }
-    return (v & 1) ? launch_k3<K, kSeg, U, 1, NA, CHAIN>(red, a, s)
-                   : launch_k3<K, kSeg, U, 0, NA, CHAIN>(red, a, s);
-}
-
-template <int K, int NA, bool CHAIN, bool RED, int NT>
-int seg_blocks_per_cu_v() {
-    int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mm_passk_kernel<K, kSeg, seg_prefetch<NA>(), RED, NT, NA, CHAIN>, kBlock, 0);
-    return e == hipSuccess ? n : 0;
-}
-
-template <int K, int NA, bool CHAIN>
-int seg_blocks_per_cu(bool red, int nt) {
-    if (red)
-        return nt ? seg_blocks_per_cu_v<K, NA, CHAIN, true, 1>()
-                  : seg_blocks_per_cu_v<K, NA, CHAIN, true, 0>();
-    return nt ? seg_blocks_per_cu_v<K, NA, CHAIN, false, 1>()
-              : seg_blocks_per_cu_v<K, NA, CHAIN, false, 0>();
-}
 
 // Fixed-order sums of the levels in `mask` of partials[n][k][na] -> one history entry of
 // na sums per level, slots from the device counter (graph-replayable).
@@ -660,36 +58,22 @@ long long passk_max_rows(int k, long long pitch) {
 }
 
 int passk_waves_per_cu(int k, int na, bool red, int nt) {
-    int b = 0;
-    switch (na * 10 + k) {
-        case 11: b = seg_blocks_per_cu<1, 1, false>(red, nt); break;
-        case 12: b = seg_blocks_per_cu<2, 1, false>(red, nt); break;
-        case 13: b = seg_blocks_per_cu<3, 1, false>(red, nt); break;
-        case 14: b = seg_blocks_per_cu<4, 1, false>(red, nt); break;
-        case 21: b = seg_blocks_per_cu<1, 2, true>(red, nt); break;
-        case 22: b = seg_blocks_per_cu<2, 2, true>(red, nt); break;
-        case 31: b = seg_blocks_per_cu<1, 3, true>(red, nt); break;
-        case 32: b = seg_blocks_per_cu<2, 3, true>(red, nt); break;
-        case 41: b = seg_blocks_per_cu<1, 4, true>(red, nt); break;
-        case 42: b = seg_blocks_per_cu<2, 4, true>(red, nt); break;
-        default: break;
+    switch (k) {
+        case 1: return passk_waves_k1(na, red, nt);
+        case 2: return passk_waves_k2(na, red, nt);
+        case 3: return passk_waves_k3(na, red, nt);
+        case 4: return passk_waves_k4(na, red, nt);
+        default: return 0;
     }
-    return b * kWavesPerBlock;
 }
 
 hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t s, int variant) {
     if (a.waves_total <= 0) return hipSuccess;
-    switch (na * 10 + k) {
-        case 11: return launch_k2<1, 1, false>(red, a, s, variant);
-        case 12: return launch_k2<2, 1, false>(red, a, s, variant);
-        case 13: return launch_k2<3, 1, false>(red, a, s, variant);
-        case 14: return launch_k2<4, 1, false>(red, a, s, variant);
-        case 21: return launch_k2<1, 2, true>(red, a, s, variant);
-        case 22: return launch_k2<2, 2, true>(red, a, s, variant);
-        case 31: return launch_k2<1, 3, true>(red, a, s, variant);
-        case 32: return launch_k2<2, 3, true>(red, a, s, variant);
-        case 41: return launch_k2<1, 4, true>(red, a, s, variant);
-        case 42: return launch_k2<2, 4, true>(red, a, s, variant);
+    switch (k) {
+        case 1: return passk_launch_k1(na, red, a, s, variant);
+        case 2: return passk_launch_k2(na, red, a, s, variant);
+        case 3: return passk_launch_k3(na, red, a, s, variant);
+        case 4: return passk_launch_k4(na, red, a, s, variant);
         default: return hipErrorInvalidValue;
     }
 }

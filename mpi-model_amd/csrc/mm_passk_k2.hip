@@ -1,0 +1,26 @@
+// mm_passk_k2.hip -- instances of the K-step kernel (mm_passk.hpp) for K = 2.
+#include "mm_passk.hpp"
+
+namespace mm {
+
+hipError_t passk_launch_k2(int na, bool red, const PassArgs& a, hipStream_t s, int v) {
+    switch (na) {
+        case 1: return launch_k2<2, 1, false>(red, a, s, v);
+        case 2: return launch_k2<2, 2, true>(red, a, s, v);
+        case 3: return launch_k2<2, 3, true>(red, a, s, v);
+        case 4: return launch_k2<2, 4, true>(red, a, s, v);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+int passk_waves_k2(int na, bool red, int nt) {
+    switch (na) {
+        case 1: return seg_blocks_per_cu<2, 1, false>(red, nt) * kWavesPerBlock;
+        case 2: return seg_blocks_per_cu<2, 2, true>(red, nt) * kWavesPerBlock;
+        case 3: return seg_blocks_per_cu<2, 3, true>(red, nt) * kWavesPerBlock;
+        case 4: return seg_blocks_per_cu<2, 4, true>(red, nt) * kWavesPerBlock;
+        default: return 0;
+    }
+}
+
+}  // namespace mm

@@ -52,7 +52,8 @@ class Info(ctypes.Structure):
     _fields_ = [("pitch", ctypes.c_longlong), ("bytes_device", ctypes.c_longlong),
                 ("n_passes", ctypes.c_int), ("rows_per_wave", ctypes.c_int),
                 ("waves_per_pass", ctypes.c_longlong), ("steps_done", ctypes.c_longlong),
-                ("fused_attrs", ctypes.c_int), ("steps_per_launch", ctypes.c_int)]
+                ("fused_attrs", ctypes.c_int), ("steps_per_launch", ctypes.c_int),
+                ("kernel", ctypes.c_int)]
 
 
 _lib = None

@@ -30,6 +30,24 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
 
 
+MPI_HOME = os.environ.get("MM_MPI_HOME", "/opt/conda")
+CPU_MPI_PATH = os.path.join(HERE, "_build", "mm_cpu_mpi")
+
+
+def cpu_mpi(H, W, rate, seconds, ranks, maxsteps=100000, dump=None, timeout=600):
+    """Run the MPI CPU baseline (mm_cpu_mpi.c: row slabs, one rank per core, blocking
+    border-row exchange, the oracle's step) as a child process; returns its JSON dict."""
+    import json
+    if not os.path.exists(CPU_MPI_PATH):
+        subprocess.run(["make", "-s", "-C", HERE, "cpu_mpi"], check=True)
+    cmd = [os.path.join(MPI_HOME, "bin", "mpirun"), "-np", str(ranks), CPU_MPI_PATH,
+           str(H), str(W), repr(float(rate)), repr(float(seconds)), str(maxsteps)]
+    if dump:
+        cmd.append(dump)
+    r = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def lib():
     global _lib
     if _lib is None:

@@ -6,6 +6,7 @@ pin the C restatement (oracle/mm_oracle.c) to fixtures produced by the reference
 itself (tests/golden/make_golden.py), then check the generalised step's invariants.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -112,6 +113,20 @@ def test_slab_decomposition_is_bit_exact(O, H, G):
         vg[lo - (x0 - 1):hi - (x0 - 1)] = v[lo:hi]
         parts.append(O.field_step_slab(H, W, x0, vg, 0.1))
     assert np.array_equal(np.vstack(parts), want)
+
+
+@pytest.mark.parametrize("H,W,P,steps", [(37, 29, 3, 5), (16, 130, 4, 3), (9, 7, 2, 4)])
+def test_cpu_mpi_baseline_is_the_oracle(O, tmp_path, H, W, P, steps):
+    """The MPI CPU baseline (oracle/mm_cpu_mpi.c, bench.py's cpu_baseline leg) reproduces the
+    oracle's whole-grid steps bit for bit across its row slabs and border-row exchange."""
+    if not os.path.exists(os.path.join(O.MPI_HOME, "bin", "mpirun")):
+        pytest.skip("no MPI")
+    out = tmp_path / "grid.bin"
+    r = O.cpu_mpi(H, W, 0.1, 0, P, maxsteps=-steps, dump=str(out), timeout=120)
+    assert r["ranks"] == P and r["steps"] == steps
+    got = np.fromfile(out, dtype=np.float64).reshape(H, W)
+    want = O.field_step(O.fill_random(H, W), 0.1, steps=steps)
+    assert np.array_equal(got, want)
 
 
 def test_program_step_conserves_total(O):
