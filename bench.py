@@ -118,6 +118,39 @@ def cpu_baseline(H, W, seconds):
                       f"or_field_step (scalar C, -O2, no MPI found), {el:.1f} s"}
 
 
+def cpu_baseline_program(H, W, na, flows, seconds):
+    """C5's CPU baseline: the oracle's scalar flow-program step (oracle/mm_oracle.c
+    or_program_step: transfers in declared order, then the diffusions) plus the per-step
+    attribute sums, one core, as many whole steps as fit in about `seconds`."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import ctypes
+    import numpy as np
+    fields = [oracle.fill_random(H, W, seed=oracle.SEED + a) for a in range(na)]
+    arr = (ctypes.c_void_p * na)(*[f.ctypes.data for f in fields])
+    fl = (oracle.OrFlow * len(flows))(*[oracle.OrFlow(*f) for f in flows])
+    scratch = np.empty((H, W), dtype=np.float64)
+    L = oracle.lib()
+
+    def step():
+        L.or_program_step(H, W, na, arr, fl, len(flows), oracle._ptr(scratch))
+        return [float(np.sum(f, dtype=np.float64)) for f in fields]
+
+    step()  # untimed warm-up
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 1000:
+            break
+    return {"value": H * W * steps / el / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
+            "sample": f"{steps} steps of the {H}x{W} grid with {na} fp64 attributes and the "
+                      f"C5 flow program + per-step sums, oracle/mm_oracle.c or_program_step "
+                      f"(scalar C, one core), {el:.1f} s"}
+
+
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
@@ -261,7 +294,8 @@ def main():
         }
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
-                if na == 1 else None
+                if na == 1 else cpu_baseline_program(wl["rows"], W, na, C5_FLOWS,
+                                                     args.cpu_seconds)
         print(json.dumps(line), flush=True)
     eng.close()
     if N > 1:
