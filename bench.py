@@ -3,12 +3,12 @@
 
 metric  : cell-updates/s (GCUPS) of the generalised Exponencial flow step
           (BASELINE.json), whole job over all ranks, + % of the HBM roofline
-workload: default "c2" = BASELINE.json configs[1]: 4096 x 4096 fp64 cells per GPU,
-          one Exponencial flow (rate 0.1, src/Main.cpp:33), 1000 steps. With
-          --gpus N the grid is (4096*N) x 4096, one row slab per GPU, border rows
-          exchanged over RCCL every step (weak scaling). Other workloads:
-          c3 (32768^2 strong), c4 (16384^2 per GPU, weak), c5 (4 attributes,
-          chained transfers + 4 diffusions, per-step sums).
+workload: default "c3" = BASELINE.json configs[2], the north_star grid: 32768 x 32768 fp64
+          cells, one Exponencial flow (rate 0.1, src/Main.cpp:33). With --gpus N the
+          grid is cut into N row slabs, one per GPU, with the border rows exchanged over
+          RCCL every K steps (strong scaling). Other workloads: c2 (4096^2 per GPU, weak:
+          Infinity-Cache resident), c4 (16384^2 per GPU, weak), c5 (4 attributes, chained
+          transfers + 4 diffusions, per-step sums).
 step    : one pass of the flow over the whole grid (all passes of the program).
 timing  : W untimed warmup steps, then exactly K steps on the production path (hipGraph
           replay of K-step kernel passes) bracketed by a barrier and a device-wide
@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--self-halo", action="store_true",
                     help="N=1 only: run the RCCL halo path against itself (MM_SELF_HALO) to "
@@ -119,11 +119,24 @@ def cpu_baseline(H, W, seconds):
 
 
 def cpu_baseline_program(H, W, na, flows, seconds):
-    """C5's CPU baseline: the oracle's scalar flow-program step (oracle/mm_oracle.c
-    or_program_step: transfers in declared order, then the diffusions) plus the per-step
-    attribute sums, one core, as many whole steps as fit in about `seconds`."""
+    """C5's CPU baseline: the same reference decomposition as cpu_baseline (row slabs, one
+    MPI rank per core, blocking border-row exchange before every diffusion) running the
+    oracle's flow program (or_program_step's semantics) plus the per-step attribute sums
+    combined in rank order (src/Model.hpp:88-92). Without an MPI: the scalar single-core
+    or_program_step."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
+    ranks = cpu_ranks()
+    if os.path.exists(os.path.join(oracle.MPI_HOME, "bin", "mpirun")):
+        r = oracle.cpu_mpi(H, W, RATE, seconds, ranks, timeout=max(120, 10 * seconds),
+                           program=flows)
+        return {"value": r["GCUPS"], "unit": "GCUPS", "cores": r["ranks"], "kind": "port",
+                "sample": f"{r['steps']} timed steps (after {r['warmup_steps']} untimed) of the "
+                          f"{H}x{W} grid with {r['n_attr']} fp64 attributes and the C5 flow "
+                          f"program ({r['n_flows']} flows) + per-step sums, {r['ranks']} MPI "
+                          f"ranks x 1 core, row slabs + blocking border-row MPI_Sendrecv before "
+                          f"every diffusion (the reference's decomposition), oracle step "
+                          f"(oracle/mm_cpu_mpi.c, -O3), {r['seconds']:.1f} s"}
     import ctypes
     import numpy as np
     fields = [oracle.fill_random(H, W, seed=oracle.SEED + a) for a in range(na)]
@@ -148,7 +161,7 @@ def cpu_baseline_program(H, W, na, flows, seconds):
     return {"value": H * W * steps / el / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
             "sample": f"{steps} steps of the {H}x{W} grid with {na} fp64 attributes and the "
                       f"C5 flow program + per-step sums, oracle/mm_oracle.c or_program_step "
-                      f"(scalar C, one core), {el:.1f} s"}
+                      f"(scalar C, one core, no MPI found), {el:.1f} s"}
 
 
 def main():
@@ -235,6 +248,12 @@ def main():
     n_launch, kern_ms, bytes_per_launch = eng.timing()
     eng.set_timing(False)
     info = eng.info()
+    if info["graph_state"] == 1:
+        path = f"hipGraph replay ({info['graph_launches']} graph launches)"
+    elif info["graph_state"] == -1:
+        path = f"eager launches: graph capture refused ({info['graph_note']})"
+    else:
+        path = "eager launches (no graph)"
 
     cells = H * W
     gcups = cells * args.steps / el / 1e9
@@ -242,7 +261,7 @@ def main():
         kern_avg_ms = kern_ms / max(n_launch, 1)
         launches_per_step = n_launch / max(args.steps, 1)
         spl = info["steps_per_launch"]
-        kname = ("mm_pass_kernel", "mm_pass2_kernel", "mm_passk_kernel")[info["kernel"]]
+        kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel"}[info["kernel"]]
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         traffic = None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -268,7 +287,7 @@ def main():
             "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
                     "seed 0x4D50494D, generated on the device",
             "config": {"workload": f"{args.workload}: {wl['desc']}", "grid": [H, W],
-                       "path": f"hipGraph replay, {kname}, {spl} fused step(s) per kernel pass",
+                       "path": f"{path}, {kname}, {spl} fused step(s) per kernel pass",
                        "rows_per_gpu": h, "n_attr": na, "rate": RATE,
                        "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else "")
                        + (" (self-halo: RCCL exchange with itself)" if args.self_halo else ""),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 1
+#define MM_ABI_VERSION 2
 
 enum mm_status {
     MM_OK = 0,
@@ -87,7 +87,15 @@ typedef struct mm_info {
     long long steps_done;      /* steps run since the last fill/upload */
     int fused_attrs;           /* attributes carried per fused pass */
     int steps_per_launch;      /* steps fused per kernel pass (temporal blocking), 1..4 */
-    int kernel;                /* step kernel: 0 mm_pass_kernel, 1 mm_pass2_kernel, 2 mm_passk_kernel */
+    int kernel;                /* step kernel: 0 mm_pass_kernel (one step per pass),
+                                  2 mm_passk_kernel (steps_per_launch steps per pass) */
+    int halo_depth;            /* ghost rows one border exchange fills (= steps per pass) */
+    int graph_state;           /* 0 no graph used yet, 1 steps replayed as hipGraphs,
+                                  -1 stream capture refused: steps run eagerly (graph_note) */
+    int graph_count;           /* hipGraphs instantiated so far */
+    long long graph_launches;  /* hipGraphLaunch calls so far */
+    long long hist_entries;    /* step-sum history entries enqueued (MPI_Report) */
+    char graph_note[160];      /* why capture was refused ("" otherwise) */
 } mm_info;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -120,13 +128,17 @@ int mm_device_synchronize(int device);
 
 /* ---- engine ------------------------------------------------------------- */
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
- * init loop (src/Model.hpp:154-157): device buffers are (h+4) x pitch fp64 per
- * attribute (two ghost rows above and below), two of them (Jacobi ping-pong).
- * Environment: MM_FUSE=0 disables the fused two-step kernel, MM_GRAPH=0 the hipGraph
- * replay, MM_ROWS_PER_WAVE (8/16/32), MM_ROWS_PER_WAVE2 (8/16, fused) and
- * MM_KERNEL_VARIANT (non-temporal policy) override tuning; MM_SELF_HALO=1 with
- * MM_HALO_RCCL and nranks == 1 makes the rank exchange border rows with itself
- * (ghost rows outside the grid: exercises the RCCL path, result unchanged). */
+ * init loop (src/Model.hpp:154-157): device buffers are (h+8) x pitch fp64 per
+ * attribute (kGhost = 4 ghost rows above and below), two of them (Jacobi ping-pong).
+ * With nranks > 1 the steps per kernel pass (and so the halo depth) are capped by the
+ * thinnest slab of the chain: RCCL engines all-reduce it at creation; host-transport
+ * engines assume mm_partition_rows slabs (floor(H/nranks) rows at least).
+ * Environment: MM_PASSK=0 (or MM_FUSE=0) runs one step per kernel pass, MM_GRAPH=0
+ * disables the hipGraph replay, MM_STEPS_PER_PASS (1..4), MM_ROWS_PER_WAVE (8/16/32),
+ * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal policy)
+ * override tuning; MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
+ * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
+ * path, result unchanged). */
 int mm_engine_create(const mm_desc* desc, mm_engine** out);
 int mm_engine_destroy(mm_engine* eng);
 int mm_engine_info(mm_engine* eng, mm_info* info);
@@ -150,11 +162,14 @@ int mm_point_apply(mm_engine* eng, int attr, long long sx, long long sy,
                    double captured, double rate);
 
 /* Run nsteps steps of the flow program (the commented-out time loop,
- * src/Model.hpp:180-183, made real). Every reduce_every-th step (0 = never) the
- * per-attribute sums of the owned cells are reduced on the device and appended
- * to the engine's history (src/Model.hpp:237-243 per-rank sum; MPI_Report).
- * Asynchronous: returns once the work is enqueued. MM_HALO_HOST engines with
- * nranks > 1 accept nsteps == 1 only (the caller exchanges between steps). */
+ * src/Model.hpp:180-183, made real). Every reduce_every-th step (0 = never; steps
+ * counted from the last mm_fill / mm_upload, across mm_run calls) the per-attribute
+ * sums of the owned cells are reduced on the device and appended to the engine's
+ * history (src/Model.hpp:237-243 per-rank sum; MPI_Report); the history grows as
+ * needed. Asynchronous: returns once the work is enqueued. MM_HALO_HOST engines with
+ * nranks > 1 run one-pass programs only and at most info.halo_depth steps per call:
+ * the caller exchanges halo_depth rows (mm_halo_export_rows / mm_halo_import_rows)
+ * between calls, and the engine runs the same interior / border split as with RCCL. */
 int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
 int mm_synchronize(mm_engine* eng);
 
@@ -165,15 +180,19 @@ int mm_sums(mm_engine* eng, double* out_per_attr);
 int mm_sums_history(mm_engine* eng, double* out, long long max_entries, long long* n);
 int mm_clear_history(mm_engine* eng);
 
-/* MM_HALO_HOST transport: copy this slab's first/last owned rows of every
- * attribute out (top/bottom: n_attr*W doubles each), and the neighbours' rows
- * into the ghost rows (NULL = no neighbour on that side). Replaces the
- * scalar halo messages src/Model.hpp:202-204 <-> :228-230 with whole rows. */
+/* MM_HALO_HOST transport: copy this slab's first/last nrows owned rows of every
+ * attribute out (top/bottom: n_attr*nrows*W doubles each, [attr][row][col]), and the
+ * neighbours' rows into the nrows ghost rows above / below (NULL = no neighbour on
+ * that side). nrows is info.halo_depth (1..4). Replaces the scalar halo messages
+ * src/Model.hpp:202-204 <-> :228-230 with whole rows. mm_halo_export/import move one
+ * row (nrows = 1). */
+int mm_halo_export_rows(mm_engine* eng, int nrows, double* top, double* bottom);
+int mm_halo_import_rows(mm_engine* eng, int nrows, const double* top, const double* bottom);
 int mm_halo_export(mm_engine* eng, double* top, double* bottom);
 int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
 
 /* Test/debug: copy nrows rows starting at local row row0 (owned rows are 0..h-1, ghost
- * rows -2..-1 and h..h+1) of the current buffer of one attribute to host (W each). */
+ * rows -4..-1 and h..h+3) of the current buffer of one attribute to host (W each). */
 int mm_debug_read_rows(mm_engine* eng, int attr, long long row0, long long nrows, double* host);
 
 /* Measurement: with timing on, mm_run records a HIP event pair around every

@@ -1,16 +1,18 @@
 // mm_engine.hip -- the host engine behind include/mpimodel.h (C ABI).
 //
 // One engine = one row slab of the global grid on one GPU:
-//   * device memory: per attribute two (h+4) x pitch fp64 buffers (Jacobi
-//     ping-pong) with two ghost rows above and below, pitch a multiple of 128;
-//   * a single-attribute, single-diffusion program runs two steps per kernel pass
-//     (mm_pass2_kernel, temporal blocking: half the HBM traffic per cell-update);
-//   * a compute stream and a comm stream; with MM_HALO_RCCL each pass first
-//     exchanges border rows with ncclSend/ncclRecv on the comm stream while the
-//     interior rows run on the compute stream, then the two border rows run;
-//   * steps are captured once into a hipGraph (one ping-pong cycle, RCCL
-//     calls included) and replayed;
-//   * per-step sums (MPI_Report) are reduced on the device into a history.
+//   * device memory: per attribute two (h + 2*kGhost) x pitch fp64 buffers (Jacobi
+//     ping-pong) with kGhost ghost rows above and below, pitch a multiple of 128;
+//   * a one-pass flow program runs K steps per kernel pass (mm_passk_kernel, temporal
+//     blocking: 16/K B of HBM traffic per cell-update); other programs run one step
+//     per pass (mm_pass_kernel);
+//   * a compute stream and a comm stream; with a halo (RCCL or host transport) each pass
+//     runs the interior rows on the compute stream while the `depth` border rows wait
+//     for the exchange on the comm stream (RCCL: ncclSend/ncclRecv of `depth` rows to
+//     both neighbours; host: the caller imported them before mm_run);
+//   * steps are captured once into a hipGraph (one ping-pong cycle, RCCL calls
+//     included) and replayed; a refused capture is reported by mm_engine_info;
+//   * per-step sums (MPI_Report) are reduced on the device into a growable history.
 // The reference's per-worker body this replaces is src/Model.hpp:135-261.
 #include <rccl/rccl.h>
 
@@ -81,6 +83,7 @@ struct mm_engine {
     int na = 1;
     long long pitch = 0;
     long long rows_alloc = 0;  // h + 2 * kGhost
+    long long min_rows = 0;    // thinnest slab of the chain: bounds the halo depth
     double* base = nullptr;
     size_t bytes = 0;
     double* buf[2][mm::kMaxAttr] = {};
@@ -90,15 +93,14 @@ struct mm_engine {
     hipEvent_t ev_comp_mark = nullptr, ev_comm_done = nullptr;
     bool comm_live = false;  // border work of this run is pending on the comm stream
     ncclComm_t comm = nullptr;
-    bool split = false;  // interior / border split (RCCL halo)
+    bool split = false;  // interior / border split (RCCL or host halo)
 
     std::vector<FlowDesc> flows;
     std::vector<Pass> passes;
 
-    int th = 8;       // rows per wave, one-step kernel
-    int th2 = 16;     // rows per wave, fused two-step kernel (MM_PASSK=0)
-    bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: older kernels)
-    int kpass = 4;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..4)
+    int th = 8;              // rows per wave, one-step kernel
+    bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
+    int kpass = 4;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
     double seg_waves = 2.0;  // segment waves per resident wave slot (MM_SEG_WAVES)
     double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
@@ -113,16 +115,20 @@ struct mm_engine {
     double* hist = nullptr;
     unsigned long long* hist_n = nullptr;
     long long hist_cap = 0;
+    long long hist_host = 0;    // entries the enqueued work appends (host-side count)
     double* sum_tmp = nullptr;  // mm_sums scratch: nblocks partials + 1 result per attribute
     long long sum_blocks = 0;
 
     long long steps_done = 0;
 
-    // graph cache: key = (parity, length, reduce_every)
-    std::map<std::tuple<int, long long, long long>, hipGraphExec_t> graphs;
+    // graph cache: key = (parity, length, reduce_every, reduction phase)
+    std::map<std::tuple<int, long long, long long, long long>, hipGraphExec_t> graphs;
 
-    bool fuse_ok = true;    // MM_FUSE=0 disables the two-step kernel
-    bool graphs_ok = true;  // MM_GRAPH=0 (or a refused capture) runs steps eagerly
+    bool graphs_ok = true;      // MM_GRAPH=0 (or a refused capture) runs steps eagerly
+    int graph_state = 0;        // 0 none yet, 1 replaying, -1 capture refused
+    long long graph_launches = 0;
+    int graph_count = 0;
+    std::string graph_note;
 
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -226,27 +232,24 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
-// Launch a pass (fused == 0), a fused two-step pass (fused == 1, `red` = its RED mode)
-// or, with kpass > 0, a K-step pass (mm_passk_kernel, red != 0: per-level sums) covering
-// `rows` rows, with an event pair around it when timing. Algorithmic bytes: every cell of
-// those rows read once and written once per attribute the launch carries.
-int launch_timed(mm_engine* e, bool fused, int red, const mm::PassArgs& A, long long rows,
-                 bool time_it, int kpass = 0) {
+// Launch a one-step pass (kpass == 0) or a K-step pass (mm_passk_kernel) covering `rows`
+// rows on the compute stream, with an event pair around it when timing. Algorithmic
+// bytes: every cell of those rows read once and written once per attribute.
+int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, bool time_it,
+                 int kpass) {
     hipEvent_t a = nullptr, b = nullptr;
     if (time_it) {
         a = next_event(e);
         b = next_event(e);
         if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
         e->ev_bytes.resize(e->ev_used / 2);
-        e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * ((fused && kpass == 0) ? 1 : e->na);
+        e->ev_bytes.back() = 16.0 * (double)rows * (double)e->d.W * e->na;
         MM_HIP(hipEventRecord(a, e->s_comp));
     }
     if (kpass > 0)
-        MM_HIP(mm::launch_passk(kpass, e->na, red != 0, A, e->s_comp, e->variant));
-    else if (fused)
-        MM_HIP(mm::launch_pass2(red, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else
-        MM_HIP(mm::launch_pass(e->na, red != 0, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
     return MM_OK;
 }
@@ -258,7 +261,8 @@ long long nstrips_k(const mm_engine* e, int k) {
 
 // Border-row exchange with both neighbours in one RCCL group: the first / last `depth`
 // owned rows go to rank-1 / rank+1, their rows land in the ghost rows. Rows are
-// contiguous (pitch doubles each), so every message is one contiguous block.
+// contiguous (pitch doubles each), so every message is one contiguous block. The
+// engine keeps depth <= min_rows, so the sent rows are always owned rows.
 int halo_rccl(mm_engine* e, int depth) {
     const int r = e->d.rank, n = e->d.nranks;
     const long long P = e->pitch, h = e->d.h;
@@ -290,18 +294,10 @@ int halo_rccl(mm_engine* e, int depth) {
     return MM_OK;
 }
 
-int begin_halo(mm_engine* e, int depth) {
-    MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
-    MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
-    MM_TRY(halo_rccl(e, depth));
-    MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
-    return MM_OK;
-}
+bool rccl_halo(const mm_engine* e) { return e->comm != nullptr; }
 
 // Rows [lo, hi) of the slab as range a, optional [lo2, hi2) as range b (A.th set).
-void set_ranges(const mm_engine* e, mm::PassArgs& A, long long lo, long long hi, long long lo2,
-                long long hi2) {
-    (void)e;
+void set_ranges(mm::PassArgs& A, long long lo, long long hi, long long lo2, long long hi2) {
     A.ra0 = (int)lo;
     A.ra1 = (int)hi;
     A.rb0 = (int)lo2;
@@ -310,75 +306,79 @@ void set_ranges(const mm_engine* e, mm::PassArgs& A, long long lo, long long hi,
     A.waves_total = A.waves_a + waves_for(A.nstrips, hi2 - lo2, A.th);
 }
 
-// One kernel pass over the slab, with the halo of `depth` rows exchanged first. With the
-// RCCL halo the interior rows (which need no ghost row) run while the rows are in flight,
-// then the `depth` border rows on each side. `entries` history entries of n_attr sums
-// are appended when red != 0 (fused: red 1 -> 1 entry, red 2 -> 2 entries).
-int enqueue_pass(mm_engine* e, const Pass& p, bool fused, int red, bool time_it) {
-    const long long h = e->d.h;
-    const int depth = fused ? 2 : 1;
-    const int entries = (fused && red == 2) ? 2 : 1;
-    const int per_wave = fused ? entries : e->na;
-    mm::PassArgs A;
-    fill_args(e, p, A);
-    if (fused) A.th = e->th2;
-    long long total_waves = 0;
-    if (e->split && h >= 2 * depth + 1) {
-        // Two streams per pass, joined by events:
-        //   comm:    halo exchange k (right after border k-1) -> [after interior k-1] border k
-        //   compute: [after border k-1] interior k
-        // so the exchange and the border rows run beside the interior kernels. Interior k
-        // reads rows written by border k-1; border k reads rows written by interior k-1
-        // and writes rows interior k-1 read; ghost rows are only touched on comm; the
-        // rows an exchange sends were written by the border kernel before it.
-        if (e->comm_live) {
-            // interior k reads the rows border k-1 wrote
-            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
-        } else {
-            // first split pass of the run: the exchange follows all earlier compute work
-            MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
-            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
-        }
-        // the exchange needs only border k-1 (same stream): it overlaps interior k-1
-        MM_TRY(halo_rccl(e, depth));
-        // border k reads rows interior k-1 wrote (and reuses the partials finalize k-1 read)
+// Start of a split pass. Two streams per pass, joined by events:
+//   comm:    [RCCL exchange k (right after border k-1)] -> [after interior k-1] border k
+//   compute: [after border k-1] interior k
+// so the exchange and the border rows run beside the interior kernels. Interior k reads
+// rows border k-1 wrote; border k reads rows interior k-1 wrote and writes rows interior
+// k-1 read; ghost rows are only touched on comm; the rows an exchange sends were written
+// by the border kernel before it. With the host transport the caller has already put the
+// neighbours' rows into the ghost rows, and the same schedule runs without the exchange.
+int split_begin(mm_engine* e, int depth) {
+    if (e->comm_live) {
+        MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+    } else {
+        // first split pass of the run: the border work follows all earlier compute work
         MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
         MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
-        set_ranges(e, A, depth, h - depth, 0, 0);
+    }
+    if (rccl_halo(e)) MM_TRY(halo_rccl(e, depth));  // needs only border k-1 (same stream)
+    // border k reads rows interior k-1 wrote (and reuses the partials finalize k-1 read)
+    MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+    MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
+    return MM_OK;
+}
+
+// Slab too thin to split: exchange first, then one launch on the compute stream.
+int unsplit_halo(mm_engine* e, int depth) {
+    if (!rccl_halo(e)) return MM_OK;
+    MM_HIP(hipEventRecord(e->ev_ready, e->s_comp));
+    MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_ready, 0));
+    MM_TRY(halo_rccl(e, depth));
+    MM_HIP(hipEventRecord(e->ev_halo, e->s_comm));
+    MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
+    return MM_OK;
+}
+
+// One single-step kernel pass over the slab (1-row halo). With a halo the interior rows
+// run while the rows are in flight, then the border row on each side. One history entry
+// of n_attr sums is appended when red.
+int enqueue_pass(mm_engine* e, const Pass& p, bool red, bool time_it) {
+    const long long h = e->d.h;
+    const int depth = 1;
+    mm::PassArgs A;
+    fill_args(e, p, A);
+    long long total_waves = 0;
+    if (e->split && h >= 2 * depth + 1) {
+        MM_TRY(split_begin(e, depth));
+        set_ranges(A, depth, h - depth, 0, 0);
         const long long interior_waves = A.waves_total;
         mm::PassArgs B = A;
-        B.th = fused ? 2 : 1;  // border: short row blocks, the launch is latency-bound
-        set_ranges(e, B, 0, depth, h - depth, h);
+        B.th = 1;  // border: short row blocks, the launch is latency-bound
+        set_ranges(B, 0, depth, h - depth, h);
         B.partial_base = interior_waves;
-        if (fused)
-            MM_HIP(mm::launch_pass2(red, B, e->s_comm, e->variant));
-        else
-            MM_HIP(mm::launch_pass(e->na, red != 0, B, e->s_comm, e->variant));
+        MM_HIP(mm::launch_pass(e->na, red, B, e->s_comm, e->variant));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
-        MM_TRY(launch_timed(e, fused, red, A, h - 2 * depth, time_it));
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, 0));
         total_waves = interior_waves + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
-        if (e->split) {  // slab too thin to split: exchange first, then one launch
-            MM_TRY(begin_halo(e, depth));
-            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
-        }
-        set_ranges(e, A, 0, h, 0, 0);
+        if (e->split) MM_TRY(unsplit_halo(e, depth));
+        set_ranges(A, 0, h, 0, 0);
         A.partial_base = 0;
-        MM_TRY(launch_timed(e, fused, red, A, h, time_it));
+        MM_TRY(launch_timed(e, red, A, h, time_it, 0));
         total_waves = A.waves_total;
     }
     if (red)
-        MM_HIP(mm::launch_finalize(e->partials, total_waves, fused ? 1 : e->na, e->hist,
-                                   e->hist_n, e->hist_cap, e->s_comp, fused ? entries : 1));
-    (void)per_wave;
+        MM_HIP(mm::launch_finalize(e->partials, total_waves, e->na, e->hist, e->hist_n,
+                                   e->hist_cap, e->s_comp, 1));
     e->cur ^= 1;
     return MM_OK;
 }
 
-// Waves of a segment-scheduled range of n rows over ns strips (mm_kernels_k.hip seg_map).
+// Waves of a segment-scheduled range of n rows over ns strips (mm_passk.hpp seg_map).
 long long seg_wave_count(long long n, long long ns, long long r, long long re) {
     if (n <= 0) return 0;
     if (ns < 3) return ns * ((n + re - 1) / re);
@@ -427,38 +427,27 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
     A.xcd_remap = e->xcd;
     long long total_waves = 0;
     if (e->split && h >= 2 * depth + 1) {
-        if (e->comm_live) {
-            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
-        } else {
-            MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
-            MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
-        }
-        MM_TRY(halo_rccl(e, depth));
-        MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
-        MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
+        MM_TRY(split_begin(e, depth));
         seg_range(e, k, red, A, depth, h - depth);
         const long long interior_waves = A.waves_total;
         mm::PassArgs B = A;
         B.seg = 0;
-        B.th = 4;  // border: short row blocks, the launch is latency-bound
+        B.th = mm::kBorderRows;  // border: short row blocks, the launch is latency-bound
         B.xcd_remap = 0;
-        set_ranges(e, B, 0, depth, h - depth, h);
+        set_ranges(B, 0, depth, h - depth, h);
         B.partial_base = interior_waves;
         MM_HIP(mm::launch_passk(k, e->na, red, B, e->s_comm, 0));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
-        MM_TRY(launch_timed(e, true, red, A, h - 2 * depth, time_it, k));
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, k));
         total_waves = interior_waves + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
-        if (e->split) {
-            MM_TRY(begin_halo(e, depth));
-            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_halo, 0));
-        }
+        if (e->split) MM_TRY(unsplit_halo(e, depth));
         seg_range(e, k, red, A, 0, h);
         A.partial_base = 0;
-        MM_TRY(launch_timed(e, true, red, A, h, time_it, k));
+        MM_TRY(launch_timed(e, red, A, h, time_it, k));
         total_waves = A.waves_total;
     }
     if (red)
@@ -472,55 +461,37 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
 int enqueue_step(mm_engine* e, bool reduce, bool time_it) {
     const int np = (int)e->passes.size();
     for (int pi = 0; pi < np; ++pi)
-        MM_TRY(enqueue_pass(e, e->passes[pi], false, (reduce && pi == np - 1) ? 1 : 0, time_it));
+        MM_TRY(enqueue_pass(e, e->passes[pi], reduce && pi == np - 1, time_it));
     return MM_OK;
 }
 
-// Two steps in one fused pass; r1 / r2: reduce after the first / second step.
-int enqueue_pair(mm_engine* e, bool r1, bool r2, bool time_it) {
-    if (r1 && !r2) {  // no kernel mode for "first step only": run the steps singly
-        MM_TRY(enqueue_step(e, true, time_it));
-        return enqueue_step(e, false, time_it);
-    }
-    return enqueue_pass(e, e->passes[0], true, r1 ? 2 : (r2 ? 1 : 0), time_it);
-}
-
-// Can steps run as fused pairs? One attribute, one pass that is a single diffusion.
-bool fusable(const mm_engine* e) {
-    if (!e->fuse_ok || e->na != 1 || e->passes.size() != 1) return false;
-    const Pass& p = e->passes[0];
-    if (!p.pre.empty() || !p.post.empty() || p.diffuse_mask != 1) return false;
-    if (e->d.nranks > 1 && e->d.halo_mode != MM_HALO_RCCL) return false;
-    return e->th2 == 8 || e->th2 == 16;
-}
-
 // Can the program run on mm_passk_kernel? One pass per step (one attribute: a single
-// diffusion; several: diffusions and transfer chains), RCCL or no halo, buffer offsets
-// below 2^31.
+// diffusion; several: diffusions and transfer chains) and buffer offsets below 2^31.
 bool passk_ok(const mm_engine* e) {
-    if (!e->fuse_ok || !e->passk || e->passes.size() != 1) return false;
-    if (e->d.nranks > 1 && e->d.halo_mode != MM_HALO_RCCL) return false;
+    if (!e->passk || e->passes.size() != 1) return false;
     if (mm::passk_max_rows(mm::kMaxSteps, e->pitch) < 64) return false;
     const Pass& p = e->passes[0];
     if (e->na == 1) return p.diffuse_mask == 1 && p.pre.empty() && p.post.empty();
     return true;
 }
 
+// Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
+// past the thinnest slab of the chain (every rank sends K owned rows each way).
 int passk_steps(const mm_engine* e) {
-    return e->na == 1 ? e->kpass : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
+    int k = e->na == 1 ? e->kpass : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
+    if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
+    return std::max(1, k);
 }
 
-// Steps one kernel pass advances: K with the K-step kernel, 2 with the older fused pair
-// kernel, 1 otherwise.
-int steps_per_launch(const mm_engine* e) {
-    if (passk_ok(e)) return passk_steps(e);
-    return fusable(e) ? 2 : 1;
-}
+// Steps one kernel pass advances: K with the K-step kernel, 1 otherwise.
+int steps_per_launch(const mm_engine* e) { return passk_ok(e) ? passk_steps(e) : 1; }
+
+// Ghost rows one exchange must fill (host transport: mm_halo_export_rows / _import_rows).
+int halo_depth(const mm_engine* e) { return steps_per_launch(e); }
 
 // Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
 int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_every,
                   bool time_it) {
-    const bool fuse = fusable(e);
     long long s = first;
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
@@ -534,20 +505,8 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
             MM_TRY(enqueue_passk(e, k, mask, time_it));
             s += k;
         }
-        if (e->comm_live) {
-            MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
-            e->comm_live = false;
-        }
-        return MM_OK;
-    }
-    while (s < end) {
-        if (fuse && s + 1 < end) {
-            MM_TRY(enqueue_pair(e, red(s), red(s + 1), time_it));
-            s += 2;
-        } else {
-            MM_TRY(enqueue_step(e, red(s), time_it));
-            s += 1;
-        }
+    } else {
+        for (; s < end; ++s) MM_TRY(enqueue_step(e, red(s), time_it));
     }
     // the compute stream is the tail of every run (and of every captured graph)
     if (e->comm_live) {
@@ -566,8 +525,9 @@ long long gcd_ll(long long a, long long b) {
     return a;
 }
 
-int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_t* out) {
-    auto key = std::make_tuple(e->cur, len, reduce_every);
+int get_graph(mm_engine* e, long long len, long long reduce_every, long long phase,
+              hipGraphExec_t* out) {
+    auto key = std::make_tuple(e->cur, len, reduce_every, phase);
     auto it = e->graphs.find(key);
     if (it != e->graphs.end()) {
         *out = it->second;
@@ -575,10 +535,11 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_
     }
     const int cur0 = e->cur;
     MM_HIP(hipStreamBeginCapture(e->s_comp, hipStreamCaptureModeThreadLocal));
-    const int rc = enqueue_steps(e, 1, len, reduce_every, false);
+    const int rc = enqueue_steps(e, phase + 1, len, reduce_every, false);
     hipGraph_t g = nullptr;
     hipError_t ec = hipStreamEndCapture(e->s_comp, &g);
     e->cur = cur0;  // capture only recorded the work; the state advances at replay
+    e->comm_live = false;
     if (rc != MM_OK) {
         if (g) (void)hipGraphDestroy(g);
         return rc;
@@ -589,11 +550,12 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, hipGraphExec_
     (void)hipGraphDestroy(g);
     if (ec != hipSuccess) return fail(MM_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ec));
     e->graphs[key] = ge;
+    e->graph_count += 1;
     *out = ge;
     return MM_OK;
 }
 
-// Rows per wave of the step kernel (a compile-time row block: 8, 16 or 32). Short
+// Rows per wave of the one-step kernel (a compile-time row block: 8, 16 or 32). Short
 // blocks give the most waves in flight, which is what the memory system wants
 // (tools/sweep.py, profiles/r01): 8 by default, MM_ROWS_PER_WAVE overrides.
 int choose_th(const mm_engine* e) {
@@ -606,9 +568,9 @@ int choose_th(const mm_engine* e) {
 }
 
 int ensure_partials(mm_engine* e) {
-    // doubles: older kernels, 128-column strips x 8-row blocks with kMaxAttr sums per wave;
-    // mm_passk_kernel, segments of >= 8 rows (edge strips) plus 4-row border blocks with
-    // K x NA <= 8 sums per wave
+    // doubles: one-step kernel, 128-column strips x 8-row blocks with kMaxAttr sums per
+    // wave (+ 1-row border blocks); mm_passk_kernel, segments of >= 8 rows (edge strips)
+    // plus 4-row border blocks with K x NA <= 8 sums per wave
     long long need = (waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16) * mm::kMaxAttr;
     const long long ns = nstrips_k(e, mm::kMaxSteps);
     need = std::max(need, (ns * ((e->d.h + 7) / 8 + 4) + 16) * 8);
@@ -617,6 +579,40 @@ int ensure_partials(mm_engine* e) {
     e->partials = nullptr;
     MM_HIP(hipMalloc(&e->partials, sizeof(double) * (size_t)need));
     e->partials_cap = need;
+    return MM_OK;
+}
+
+// Make room for `more` history entries beyond the ones already enqueued. The history
+// pointer is captured by the step graphs, so growing it drops them.
+int reserve_history(mm_engine* e, long long more) {
+    const long long need = e->hist_host + more;
+    if (need <= e->hist_cap) return MM_OK;
+    const long long cap = std::max(need, 2 * e->hist_cap);
+    double* nh = nullptr;
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    MM_HIP(hipMalloc(&nh, sizeof(double) * (size_t)cap * e->na));
+    MM_HIP(hipMemcpy(nh, e->hist, sizeof(double) * (size_t)e->hist_cap * e->na,
+                     hipMemcpyDeviceToDevice));
+    (void)hipFree(e->hist);
+    e->hist = nh;
+    e->hist_cap = cap;
+    drop_graphs(e);
+    return MM_OK;
+}
+
+int copy_rows(mm_engine* e, bool to_host, long long row0, int nrows, double* host) {
+    const long long W = e->d.W, P = e->pitch;
+    for (int a = 0; a < e->na; ++a) {
+        double* dev = e->buf[e->cur][a] + row0 * P;
+        double* hp = host + (size_t)a * nrows * W;
+        if (to_host)
+            MM_HIP(hipMemcpy2DAsync(hp, sizeof(double) * W, dev, sizeof(double) * P,
+                                    sizeof(double) * W, nrows, hipMemcpyDeviceToHost, e->s_comp));
+        else
+            MM_HIP(hipMemcpy2DAsync(dev, sizeof(double) * P, hp, sizeof(double) * W,
+                                    sizeof(double) * W, nrows, hipMemcpyHostToDevice, e->s_comp));
+    }
     return MM_OK;
 }
 
@@ -714,14 +710,13 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->pitch = (d.W + mm::kStripCols - 1) / mm::kStripCols * mm::kStripCols;
     e->nstrips = (int)(e->pitch / mm::kStripCols);
     e->rows_alloc = d.h + 2 * mm::kGhost;
-    if (const char* f = std::getenv("MM_FUSE")) e->fuse_ok = std::atoi(f) != 0;
+    // thinnest slab of the chain: mm_partition_rows slabs are at least floor(H/G) rows
+    // (RCCL engines replace this with the chain's true minimum below)
+    e->min_rows = std::min<long long>(d.h, d.H / d.nranks);
     if (const char* g = std::getenv("MM_GRAPH")) e->graphs_ok = std::atoi(g) != 0;
     e->th = choose_th(e);
-    if (const char* s2 = std::getenv("MM_ROWS_PER_WAVE2")) {
-        const int v = std::atoi(s2);
-        if (v == 8 || v == 16) e->th2 = v;
-    }
-    if (const char* p = std::getenv("MM_PASSK")) e->passk = std::atoi(p) != 0;
+    if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
+    if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
         if (v >= 1 && v <= mm::kMaxSteps) e->kpass = v;
@@ -771,7 +766,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
 
     int rc = ensure_partials(e);
     if (rc != MM_OK) return cleanup(rc);
-    e->hist_cap = 1 << 16;
+    e->hist_cap = 1 << 12;
     if (hipMalloc(&e->hist, sizeof(double) * (size_t)e->hist_cap * e->na) != hipSuccess ||
         hipMalloc(&e->hist_n, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->hist_n, 0, sizeof(unsigned long long)) != hipSuccess)
@@ -799,6 +794,18 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         ncclResult_t nr = ncclCommInitRank(&e->comm, d.nranks, id, d.rank);
         if (nr != ncclSuccess)
             return cleanup(fail(MM_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr)));
+        // the chain's thinnest slab (one setup-time collective): a depth-K exchange must
+        // never send more rows than any rank owns
+        long long hmin = d.h;
+        double* dv = e->sum_tmp;
+        if (hipMemcpy(dv, &hmin, sizeof hmin, hipMemcpyHostToDevice) != hipSuccess ||
+            ncclAllReduce(dv, dv, 1, ncclInt64, ncclMin, e->comm, e->s_comm) != ncclSuccess ||
+            hipStreamSynchronize(e->s_comm) != hipSuccess ||
+            hipMemcpy(&hmin, dv, sizeof hmin, hipMemcpyDeviceToHost) != hipSuccess)
+            return cleanup(fail(MM_ERR_RCCL, "min slab rows all-reduce failed"));
+        e->min_rows = hmin;
+        e->split = true;
+    } else if (d.nranks > 1 && d.halo_mode == MM_HALO_HOST) {
         e->split = true;
     }
     // default program: one Exponencial flow on attribute 0 is set by the caller
@@ -845,13 +852,19 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         info->waves_per_pass = A.waves_total;
         info->kernel = 2;
     } else {
-        info->kernel = spl == 2 ? 1 : 0;
-        info->rows_per_wave = fusable(e) ? e->th2 : e->th;
+        info->kernel = 0;
+        info->rows_per_wave = e->th;
         info->waves_per_pass = waves_for(e, e->d.h);
     }
     info->steps_done = e->steps_done;
     info->fused_attrs = e->na;
     info->steps_per_launch = spl;
+    info->halo_depth = halo_depth(e);
+    info->graph_state = e->graph_state;
+    info->graph_count = e->graph_count;
+    info->graph_launches = e->graph_launches;
+    info->hist_entries = e->hist_host;
+    std::snprintf(info->graph_note, sizeof info->graph_note, "%s", e->graph_note.c_str());
     return MM_OK;
 }
 
@@ -937,43 +950,62 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     if (nsteps == 0) return MM_OK;
     if (e->passes.empty()) return fail(MM_ERR_STATE, "mm_run: no flow added (mm_add_flow)");
     if (e->d.halo_mode == MM_HALO_HOST && e->d.nranks > 1) {
-        if (nsteps != 1 || e->passes.size() != 1)
-            return fail(MM_ERR_STATE, "mm_run: host halo transport runs one single-pass step per call");
+        if (e->passes.size() != 1)
+            return fail(MM_ERR_STATE, "mm_run: the host halo transport runs one-pass flow programs only");
+        if (nsteps > halo_depth(e))
+            return fail(MM_ERR_STATE, "mm_run: host halo transport: at most halo_depth steps per "
+                                      "call (exchange halo_depth rows between calls)");
     }
     MM_TRY(set_device(e));
+    // steps are numbered from the last fill / upload on, so a run split into several
+    // calls reduces the same steps as one call
+    const long long phase = reduce_every > 0 ? e->steps_done % reduce_every : 0;
+    const long long entries =
+        reduce_every > 0 ? (phase + nsteps) / reduce_every - phase / reduce_every : 0;
+    MM_TRY(reserve_history(e, entries));
     const int np = (int)e->passes.size();
-    if (e->timing) {  // eager launches with an event pair around each step kernel
-        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, true));
+    auto finish = [&]() {
         e->steps_done += nsteps;
+        e->hist_host += entries;
         return MM_OK;
+    };
+    if (e->timing) {  // eager launches with an event pair around each step kernel
+        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, true));
+        return finish();
     }
-    // Replay a graph of `per` steps: a whole number of fused pairs, an even number of
-    // buffer flips (so the captured pointers are valid again) and of reduction periods.
+    // Replay a graph of `per` steps: a whole number of K-step passes, an even number of
+    // buffer flips (so the captured pointers are valid again) and of reduction periods
+    // (so the phase is the same at every replay).
     const long long unit = steps_per_launch(e);
-    const long long flips = (passk_ok(e) || fusable(e)) ? 1 : np;
+    const long long flips = passk_ok(e) ? 1 : np;
     long long len = unit * ((flips % 2) ? 2 : 1);
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
     if (len > 256 || nsteps < len || !e->graphs_ok) {
-        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, false));
-        e->steps_done += nsteps;
-        return MM_OK;
+        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, false));
+        return finish();
     }
     long long per = len;
     while (per < 16 && per * 2 <= nsteps) per *= 2;
     hipGraphExec_t g = nullptr;
-    if (get_graph(e, per, reduce_every, &g) != MM_OK) {
-        // stream capture refused (e.g. by the RCCL build): run the same steps eagerly
+    if (get_graph(e, per, reduce_every, phase, &g) != MM_OK) {
+        // stream capture refused (e.g. by the RCCL build): run the same steps eagerly and
+        // say so in mm_engine_info (graph_state -1, graph_note)
+        e->graph_note = g_last_error;
         (void)hipGetLastError();
         e->graphs_ok = false;
-        MM_TRY(enqueue_steps(e, 1, nsteps, reduce_every, false));
-        e->steps_done += nsteps;
-        return MM_OK;
+        e->graph_state = -1;
+        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, false));
+        return finish();
     }
+    e->graph_state = 1;
     long long done = 0;
-    for (; done + per <= nsteps; done += per) MM_HIP(hipGraphLaunch(g, e->s_comp));
-    if (done < nsteps) MM_TRY(enqueue_steps(e, done + 1, nsteps - done, reduce_every, false));
-    e->steps_done += nsteps;
-    return MM_OK;
+    for (; done + per <= nsteps; done += per) {
+        MM_HIP(hipGraphLaunch(g, e->s_comp));
+        e->graph_launches += 1;
+    }
+    if (done < nsteps)
+        MM_TRY(enqueue_steps(e, phase + done + 1, nsteps - done, reduce_every, false));
+    return finish();
 }
 
 int mm_synchronize(mm_engine* e) {
@@ -1002,8 +1034,9 @@ int mm_sums_history(mm_engine* e, double* out, long long max_entries, long long*
     unsigned long long cnt = 0;
     MM_HIP(hipStreamSynchronize(e->s_comp));
     MM_HIP(hipMemcpy(&cnt, e->hist_n, sizeof cnt, hipMemcpyDeviceToHost));
-    long long avail = std::min<long long>((long long)cnt, e->hist_cap);
-    long long k = std::min(avail, max_entries);
+    if ((long long)cnt > e->hist_cap)  // reserve_history keeps this from happening
+        return fail(MM_ERR_STATE, "mm_sums_history: history overflowed its buffer");
+    const long long k = std::min((long long)cnt, max_entries);
     if (k > 0) MM_HIP(hipMemcpy(out, e->hist, sizeof(double) * (size_t)(k * e->na), hipMemcpyDeviceToHost));
     *n = (long long)cnt;
     return MM_OK;
@@ -1014,39 +1047,38 @@ int mm_clear_history(mm_engine* e) {
     MM_TRY(set_device(e));
     MM_HIP(hipStreamSynchronize(e->s_comp));
     MM_HIP(hipMemset(e->hist_n, 0, sizeof(unsigned long long)));
+    e->hist_host = 0;
+    return MM_OK;
+}
+
+int mm_halo_export_rows(mm_engine* e, int nrows, double* top, double* bottom) {
+    if (!e || nrows < 1 || nrows > e->d.h || nrows > mm::kGhost)
+        return fail(MM_ERR_INVALID, "mm_halo_export_rows: nrows must be 1..min(h, kGhost)");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    if (top) MM_TRY(copy_rows(e, true, 0, nrows, top));
+    if (bottom) MM_TRY(copy_rows(e, true, e->d.h - nrows, nrows, bottom));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
+int mm_halo_import_rows(mm_engine* e, int nrows, const double* top, const double* bottom) {
+    if (!e || nrows < 1 || nrows > mm::kGhost)
+        return fail(MM_ERR_INVALID, "mm_halo_import_rows: nrows must be 1..kGhost");
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    if (top) MM_TRY(copy_rows(e, false, -nrows, nrows, const_cast<double*>(top)));
+    if (bottom) MM_TRY(copy_rows(e, false, e->d.h, nrows, const_cast<double*>(bottom)));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
     return MM_OK;
 }
 
 int mm_halo_export(mm_engine* e, double* top, double* bottom) {
-    if (!e) return fail(MM_ERR_INVALID, "mm_halo_export: null");
-    MM_TRY(set_device(e));
-    const long long W = e->d.W, P = e->pitch, h = e->d.h;
-    for (int a = 0; a < e->na; ++a) {
-        if (top)
-            MM_HIP(hipMemcpyAsync(top + a * W, e->buf[e->cur][a], sizeof(double) * W,
-                                  hipMemcpyDeviceToHost, e->s_comp));
-        if (bottom)
-            MM_HIP(hipMemcpyAsync(bottom + a * W, e->buf[e->cur][a] + (h - 1) * P, sizeof(double) * W,
-                                  hipMemcpyDeviceToHost, e->s_comp));
-    }
-    MM_HIP(hipStreamSynchronize(e->s_comp));
-    return MM_OK;
+    return mm_halo_export_rows(e, 1, top, bottom);
 }
 
 int mm_halo_import(mm_engine* e, const double* top, const double* bottom) {
-    if (!e) return fail(MM_ERR_INVALID, "mm_halo_import: null");
-    MM_TRY(set_device(e));
-    const long long W = e->d.W, P = e->pitch, h = e->d.h;
-    for (int a = 0; a < e->na; ++a) {
-        if (top)
-            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] - P, top + a * W, sizeof(double) * W,
-                                  hipMemcpyHostToDevice, e->s_comp));
-        if (bottom)
-            MM_HIP(hipMemcpyAsync(e->buf[e->cur][a] + h * P, bottom + a * W,
-                                  sizeof(double) * W, hipMemcpyHostToDevice, e->s_comp));
-    }
-    MM_HIP(hipStreamSynchronize(e->s_comp));
-    return MM_OK;
+    return mm_halo_import_rows(e, 1, top, bottom);
 }
 
 int mm_debug_read_rows(mm_engine* e, int attr, long long row0, long long nrows, double* host) {
@@ -1091,7 +1123,7 @@ int mm_timing(mm_engine* e, long long* n, double* total_ms, double* bytes_per_la
     if (n) *n = e->timed_launches;
     if (total_ms) *total_ms = e->timed_ms;
     // algorithmic bytes of a timed launch: each cell of its rows read once and written
-    // once per attribute (16 B), whether the launch advances one step or two
+    // once per attribute (16 B), whether the launch advances one step or K
     if (bytes_per_launch)
         *bytes_per_launch = e->timed_launches ? e->timed_bytes / (double)e->timed_launches : 0.0;
     return MM_OK;

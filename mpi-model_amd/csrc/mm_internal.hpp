@@ -13,6 +13,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
 constexpr int kMaxSteps = 4;    // fused steps per pass of mm_passk_kernel
 constexpr int kGhost = kMaxSteps;  // ghost rows above and below a slab (K fused steps need K)
+constexpr int kBorderRows = 4;     // rows per wave of the K-step kernel's border launches
 
 // One fused Jacobi pass over a row slab. Every buffer pointer points at owned row 0;
 // rows -kGhost..-1 and h..h+kGhost-1 are ghost rows; local row r is global x_init+r.
@@ -45,9 +46,6 @@ struct PassArgs {
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
 hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);
-// Two fused steps of a single-attribute, single-diffusion program (mm_pass2_kernel).
-// red: 0 no sums, 1 second step's sums (partials[wave]), 2 both (partials[wave][2]).
-hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant);
 // K fused steps of a one-pass flow program (NA = 1: K 1..4, one diffusion; NA 2..4:
 // K 1..2, diffusions and transfer chains) on overlapped strips (mm_passk_kernel,
 // mm_kernels_k.hip). a.seg: segment schedule, a.th / a.th_edge rows per wave; else 4-row

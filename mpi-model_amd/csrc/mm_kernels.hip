@@ -13,11 +13,9 @@
 //     wave_shr:1 / wave_shl:1 (no LDS, no barrier); lanes 0 and 63 additionally
 //     load the one column left / right of the strip;
 //   * rows are prefetched U at a time so every wave keeps U KiB in flight.
-// mm_pass2_kernel fuses TWO steps per pass (temporal blocking): it reads each cell
-// once, computes the intermediate step for rows/columns the second step needs (one
-// extra row and column on every side, recomputed by the neighbouring wave too), and
-// writes the cell once -- 8 B of HBM traffic per cell-update instead of 16 B. Both
-// levels use exactly the single-step arithmetic, so results are bit-identical.
+// The K-step temporal-blocking kernel (the single-attribute hot path) lives in
+// mm_passk.hpp; this one-step kernel runs flow programs that need more than one pass
+// per step, and every program when MM_PASSK=0.
 // Layout: every buffer pointer points at owned row 0 of the slab; rows -kGhost..-1 and
 // h..h+kGhost-1 are ghost rows (global row = x_init + local row).
 // Arithmetic order is the contract in oracle/mm_oracle.h; the .so is built with
@@ -334,186 +332,6 @@ __global__ __launch_bounds__(kBlock) void mm_pass_kernel(const PassArgs A) {
     }
 }
 
-// ---- two fused steps (temporal blocking), one attribute, no transfers -------------
-
-// One input row as a lane sees it: its two columns and an edge PAIR (lane 0: the two
-// columns left of the strip, lane 63: the two right of it).
-struct Raw2 {
-    double v0, v1, ea, eb;
-};
-
-// Level-1 processed row: shares of the four columns and u - out of the own pair and of
-// the inner edge column (lane 0: base-1 = eb, lane 63: base+128 = ea).
-struct Proc2 {
-    double s0, s1, sa, sb, d0, d1, de;
-};
-
-template <int NT>
-__device__ __forceinline__ void load_row2(const PassArgs& A, int r, int rmax, unsigned voff,
-                                          unsigned eoff2, Raw2& o) {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(A.in[0], r, rmax, A.pitch);
-    const dv2 p = __builtin_bit_cast(
-        dv2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, (NT & 2) ? 2 : 0));
-    const dv2 e = __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(rs, eoff2, 0, 0));
-    o.v0 = p.x;
-    o.v1 = p.y;
-    o.ea = e.x;
-    o.eb = e.y;
-}
-
-__device__ __forceinline__ void process_row2(const PassArgs& A, int r, const Raw2& v,
-                                             bool fast_cols1, bool lane0, int sy0, int sy1,
-                                             int sya, int syb, Proc2& o) {
-    const int sx = span3(A.H, A.x_init + r);
-    const double rate = A.drate[0];
-    if (sx == 0) {
-        o.s0 = o.s1 = o.sa = o.sb = 0.0;
-        o.d0 = v.v0;
-        o.d1 = v.v1;
-        o.de = lane0 ? v.eb : v.ea;
-        return;
-    }
-    if (sx == 3 && fast_cols1) {
-        const double o0 = rate * v.v0, o1 = rate * v.v1, oa = rate * v.ea, ob = rate * v.eb;
-        o.s0 = o0 * 0.125;
-        o.s1 = o1 * 0.125;
-        o.sa = oa * 0.125;
-        o.sb = ob * 0.125;
-        o.d0 = v.v0 - o0;
-        o.d1 = v.v1 - o1;
-        o.de = lane0 ? v.eb - ob : v.ea - oa;
-        return;
-    }
-    const int c0 = (sx && sy0) ? sx * sy0 - 1 : 0;
-    const int c1 = (sx && sy1) ? sx * sy1 - 1 : 0;
-    const int ca = (sx && sya) ? sx * sya - 1 : 0;
-    const int cb = (sx && syb) ? sx * syb - 1 : 0;
-    const double o0 = c0 > 0 ? rate * v.v0 : 0.0;
-    const double o1 = c1 > 0 ? rate * v.v1 : 0.0;
-    const double oa = ca > 0 ? rate * v.ea : 0.0;
-    const double ob = cb > 0 ? rate * v.eb : 0.0;
-    o.s0 = share_of(o0, c0);
-    o.s1 = share_of(o1, c1);
-    o.sa = share_of(oa, ca);
-    o.sb = share_of(ob, cb);
-    o.d0 = v.v0 - o0;
-    o.d1 = v.v1 - o1;
-    o.de = lane0 ? v.eb - ob : v.ea - oa;
-}
-
-// Level-1 (intermediate step) values of the middle row: own pair + inner edge column,
-// laid out exactly as a single-step input row (RawRow<1>) for level 2.
-__device__ __forceinline__ void emit_row2(const Proc2& P, const Proc2& C, const Proc2& N,
-                                          bool lane0, RawRow<1>& u) {
-    const double p0 = P.s0 + N.s0, p1 = P.s1 + N.s1, pa = P.sa + N.sa, pb = P.sb + N.sb;
-    const double c0 = p0 + C.s0, c1 = p1 + C.s1, ca = pa + C.sa, cb = pb + C.sb;
-    const double left = dpp_from_lower_lane(c1, cb);   // lane 0: c3 at base-1 (eb)
-    const double right = dpp_from_upper_lane(c0, ca);  // lane 63: c3 at base+128 (ea)
-    u.v0[0] = C.d0 + ((left + c1) + p0);
-    u.v1[0] = C.d1 + ((c0 + right) + p1);
-    // inner edge column: lane 0 at base-1 (neighbours base-2 = ea, base = own 0),
-    // lane 63 at base+128 (neighbours base+127 = own 1, base+129 = eb)
-    u.ve[0] = C.de + (lane0 ? ((ca + c0) + pb) : ((c1 + cb) + pa));
-}
-
-// RED: 0 no sums, 1 the second step's sums, 2 both steps' sums (partials[wave][RED]).
-template <int TH, int U, int RED, int NT>
-__global__ __launch_bounds__(kBlock) void mm_pass2_kernel(const PassArgs A) {
-    static_assert(U <= TH + 2, "prefetch deeper than the row block");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long wid = (long long)blockIdx.x * kWavesPerBlock + wave;
-    if (wid >= A.waves_total) return;
-
-    int rlo, rhi;
-    long long w = wid;
-    if (w < A.waves_a) {
-        rlo = A.ra0;
-        rhi = A.ra1;
-    } else {
-        w -= A.waves_a;
-        rlo = A.rb0;
-        rhi = A.rb1;
-    }
-    const int strip = (int)(w % A.nstrips);
-    const int rb = (int)(w / A.nstrips);
-    const int rA = rlo + rb * TH;
-    const int rB = min(rA + TH, rhi);  // output rows [rA, rB); inputs [rA-2, rB+1]
-
-    const long long base = (long long)strip * kStripCols;
-    const long long y0 = base + 2 * lane;
-    const long long W = A.W;
-    const bool lane0 = lane == 0;
-    // level 1: edge pair (lane 0: base-2, base-1; lane 63: base+128, base+129)
-    const long long ya = lane0 ? base - 2 : base + kStripCols;
-    const bool pair_ok = (lane0 && base > 0) || (lane == 63 && base + kStripCols < W);
-    const int sy0 = span3(W, y0), sy1 = span3(W, y0 + 1);
-    const int sya = pair_ok ? span3(W, ya) : 0, syb = pair_ok ? span3(W, ya + 1) : 0;
-    const bool fast1 = base >= 3 && base + kStripCols + 1 <= W - 2;
-    // level 2: single edge column (lane 0: base-1, lane 63: base+128)
-    const long long ye = lane0 ? base - 1 : (lane == 63 ? base + kStripCols : -1);
-    const bool edge_ok = ye >= 0 && ye < W;
-    const int sye = edge_ok ? span3(W, ye) : 0;
-    const bool fast2 = base >= 2 && base + kStripCols <= W - 2;
-    const bool st1 = y0 < W, st2 = y0 + 1 < W;
-    const unsigned voff = (unsigned)(y0 * 8);
-    const unsigned eoff2 = pair_ok ? (unsigned)(ya * 8) : kOOB;
-
-    double acc1[1] = {0.0}, acc2[1] = {0.0};
-
-    // input i = row rA-2+i, i in [0, TH+4); inputs >= 2 rotate through raw[(i-2) % U]
-    constexpr int NI = TH + 4;
-    const int rmax = rB + 1;
-    Raw2 in0, in1, raw[U];
-    load_row2<NT>(A, rA - 2, rmax, voff, eoff2, in0);
-    load_row2<NT>(A, rA - 1, rmax, voff, eoff2, in1);
-#pragma unroll
-    for (int k = 0; k < U; ++k) load_row2<NT>(A, rA + k, rmax, voff, eoff2, raw[k]);
-    Proc2 P1, C1, N1;
-    process_row2(A, rA - 2, in0, fast1, lane0, sy0, sy1, sya, syb, P1);
-    process_row2(A, rA - 1, in1, fast1, lane0, sy0, sy1, sya, syb, C1);
-    ProcRow<1> P2, C2, N2;
-#pragma unroll
-    for (int i = 2; i < NI; ++i) {
-        process_row2(A, rA - 2 + i, raw[(i - 2) % U], fast1, lane0, sy0, sy1, sya, syb, N1);
-        if (i + U < NI) load_row2<NT>(A, rA - 2 + i + U, rmax, voff, eoff2, raw[(i - 2) % U]);
-        // level-1 row rA-3+i (j = i-2: rows rA-1 .. rA+TH)
-        const int r1 = rA - 3 + i;
-        RawRow<1> u;
-        emit_row2(P1, C1, N1, lane0, u);
-        P1 = C1;
-        C1 = N1;
-        if (RED == 2) {
-            const bool own = r1 >= rA && r1 < rB;  // wave-uniform
-            acc1[0] = acc1[0] + ((own && st1) ? u.v0[0] : 0.0);
-            acc1[0] = acc1[0] + ((own && st2) ? u.v1[0] : 0.0);
-        }
-        if (i == 2) {
-            process_row<1, false>(A, r1, u, fast2, sy0, sy1, sye, P2);
-        } else if (i == 3) {
-            process_row<1, false>(A, r1, u, fast2, sy0, sy1, sye, C2);
-        } else {
-            process_row<1, false>(A, r1, u, fast2, sy0, sy1, sye, N2);
-            emit_row<1, (RED > 0), NT, false>(A, r1 - 1, rB - 1, voff, st2, st1, P2, C2, N2, acc2);
-            copy_row<1>(P2, C2);
-            copy_row<1>(C2, N2);
-        }
-    }
-
-    if (RED > 0) {
-        const double t2 = wave_sum(acc2[0]);
-        if (RED == 2) {
-            const double t1 = wave_sum(acc1[0]);
-            if (lane == 0) {
-                A.partials[(A.partial_base + wid) * 2 + 0] = t1;
-                A.partials[(A.partial_base + wid) * 2 + 1] = t2;
-            }
-        } else if (lane == 0) {
-            A.partials[A.partial_base + wid] = t2;
-        }
-    }
-}
-
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
     z += 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -686,28 +504,6 @@ hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, in
         case 4: return launch_pass_na<4>(reduce, a, s, variant);
         default: return hipErrorInvalidValue;
     }
-}
-
-template <int TH, int U, int NT>
-hipError_t launch2_v(int red, const PassArgs& a, hipStream_t s) {
-    const long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
-    const dim3 g((unsigned)blocks), b(kBlock);
-    switch (red) {
-        case 1: hipLaunchKernelGGL((mm_pass2_kernel<TH, U, 1, NT>), g, b, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((mm_pass2_kernel<TH, U, 2, NT>), g, b, 0, s, a); break;
-        default: hipLaunchKernelGGL((mm_pass2_kernel<TH, U, 0, NT>), g, b, 0, s, a); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_pass2(int red, const PassArgs& a, hipStream_t s, int variant) {
-    if (a.waves_total <= 0) return hipSuccess;
-    // variant: non-temporal policy (0 none, 1 stores); rows per wave a.th in {8, 16},
-    // 2 for the border rows of a halo-split pass (short chains for a latency-bound launch)
-    if (a.th == 2) return launch2_v<2, 4, 0>(red, a, s);
-    if (a.th == 16) return variant == 1 ? launch2_v<16, 8, 1>(red, a, s) : launch2_v<16, 8, 0>(red, a, s);
-    if (a.th != 8) return hipErrorInvalidValue;
-    return variant == 1 ? launch2_v<8, 8, 1>(red, a, s) : launch2_v<8, 8, 0>(red, a, s);
 }
 
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,

@@ -73,6 +73,9 @@ constexpr int kSeg = 0;                  // MODE value of the segment schedule
 #endif
 
 // input rows prefetched per wave: 8 KiB in flight for one attribute, ~8 KiB for more
+#ifndef MM_FMA_SHARE
+#define MM_FMA_SHARE 0  // interior cells: s = u*(r/8), u - out = fma(s, -8, u)
+#endif
 #ifndef MM_LEVEL_BARRIER
 #define MM_LEVEL_BARRIER 0  // scheduling barrier after every this many levels (0: none)
 #endif
@@ -200,11 +203,19 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
         }
         const double r = A.drate[a];
         if (inner) {  // interior row, interior strip: cnt == 8
+#if MM_FMA_SHARE
+            const double r8 = r * 0.125;
+            s0[a] = u0[a] * r8;
+            s1[a] = u1[a] * r8;
+            d0[a] = __builtin_fma(s0[a], -8.0, u0[a]);
+            d1[a] = __builtin_fma(s1[a], -8.0, u1[a]);
+#else
             const double o0 = r * u0[a], o1 = r * u1[a];
             s0[a] = o0 * 0.125;
             s1[a] = o1 * 0.125;
             d0[a] = u0[a] - o0;
             d1[a] = u1[a] - o1;
+#endif
         } else if (sx == 0) {  // row outside the grid
             s0[a] = s1[a] = 0.0;
             d0[a] = u0[a];
@@ -601,8 +612,6 @@ __global__ __launch_bounds__(kBlock, MM_PASSK_MIN_WAVES) void mm_passk_kernel(co
                                                               soff);
     }
 }
-
-constexpr int kBorderRows = 4;  // block schedule rows (border launches)
 
 template <int K, int MODE, int U, int NT, int NA, bool CHAIN>
 hipError_t launch_k3(bool red, const PassArgs& a, hipStream_t s) {

@@ -30,7 +30,8 @@ EXPORTS = [
     "mm_comm_id_create", "mm_device_count", "mm_device_synchronize", "mm_engine_create", "mm_engine_destroy",
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
     "mm_point_apply", "mm_run", "mm_synchronize", "mm_sums", "mm_sums_history",
-    "mm_clear_history", "mm_halo_export", "mm_halo_import", "mm_debug_read_rows",
+    "mm_clear_history", "mm_halo_export_rows", "mm_halo_import_rows", "mm_halo_export",
+    "mm_halo_import", "mm_debug_read_rows",
     "mm_set_timing", "mm_timing",
 ]
 
@@ -53,7 +54,10 @@ class Info(ctypes.Structure):
                 ("n_passes", ctypes.c_int), ("rows_per_wave", ctypes.c_int),
                 ("waves_per_pass", ctypes.c_longlong), ("steps_done", ctypes.c_longlong),
                 ("fused_attrs", ctypes.c_int), ("steps_per_launch", ctypes.c_int),
-                ("kernel", ctypes.c_int)]
+                ("kernel", ctypes.c_int), ("halo_depth", ctypes.c_int),
+                ("graph_state", ctypes.c_int), ("graph_count", ctypes.c_int),
+                ("graph_launches", ctypes.c_longlong), ("hist_entries", ctypes.c_longlong),
+                ("graph_note", ctypes.c_char * 160)]
 
 
 _lib = None
@@ -94,6 +98,8 @@ def lib():
             "mm_sums": (I, [P, P]),
             "mm_sums_history": (I, [P, P, LL, pLL]),
             "mm_clear_history": (I, [P]),
+            "mm_halo_export_rows": (I, [P, I, P, P]),
+            "mm_halo_import_rows": (I, [P, I, P, P]),
             "mm_halo_export": (I, [P, P, P]),
             "mm_halo_import": (I, [P, P, P]),
             "mm_debug_read_rows": (I, [P, I, LL, LL, P]),
@@ -198,7 +204,9 @@ class Engine:
     def info(self):
         i = Info()
         check(lib().mm_engine_info(self.ptr, ctypes.byref(i)))
-        return {k: getattr(i, k) for k, _ in Info._fields_}
+        out = {k: getattr(i, k) for k, _ in Info._fields_}
+        out["graph_note"] = i.graph_note.decode(errors="replace")
+        return out
 
     def fill(self, attr=0, mode=MM_FILL_UNIFORM, value=1.0, seed=SEED):
         check(lib().mm_fill(self.ptr, attr, mode, value, seed))
@@ -248,16 +256,20 @@ class Engine:
     def clear_history(self):
         check(lib().mm_clear_history(self.ptr))
 
-    def halo_export(self):
-        top = np.empty(self.n_attr * self.W, dtype=np.float64)
-        bot = np.empty(self.n_attr * self.W, dtype=np.float64)
-        check(lib().mm_halo_export(self.ptr, _dptr(top), _dptr(bot)))
+    def halo_export(self, nrows=1):
+        """First / last nrows owned rows of every attribute: two (n_attr, nrows, W) arrays."""
+        top = np.empty((self.n_attr, nrows, self.W), dtype=np.float64)
+        bot = np.empty((self.n_attr, nrows, self.W), dtype=np.float64)
+        check(lib().mm_halo_export_rows(self.ptr, nrows, _dptr(top), _dptr(bot)))
         return top, bot
 
-    def halo_import(self, top=None, bottom=None):
+    def halo_import(self, top=None, bottom=None, nrows=1):
+        """Neighbour rows (n_attr, nrows, W) into the ghost rows above / below."""
         t = None if top is None else np.ascontiguousarray(top, dtype=np.float64)
         b = None if bottom is None else np.ascontiguousarray(bottom, dtype=np.float64)
-        check(lib().mm_halo_import(self.ptr, _dptr(t), _dptr(b)))
+        for x in (t, b):
+            assert x is None or x.size == self.n_attr * nrows * self.W
+        check(lib().mm_halo_import_rows(self.ptr, nrows, _dptr(t), _dptr(b)))
 
     def read_rows(self, row0, nrows, attr=0):
         out = np.empty((nrows, self.W), dtype=np.float64)

@@ -34,9 +34,11 @@ MPI_HOME = os.environ.get("MM_MPI_HOME", "/opt/conda")
 CPU_MPI_PATH = os.path.join(HERE, "_build", "mm_cpu_mpi")
 
 
-def cpu_mpi(H, W, rate, seconds, ranks, maxsteps=100000, dump=None, timeout=600):
+def cpu_mpi(H, W, rate, seconds, ranks, maxsteps=100000, dump=None, timeout=600, program=None):
     """Run the MPI CPU baseline (mm_cpu_mpi.c: row slabs, one rank per core, blocking
-    border-row exchange, the oracle's step) as a child process; returns its JSON dict."""
+    border-row exchange, the oracle's step) as a child process; returns its JSON dict.
+    program: [(kind, a, b, rate)] runs that flow program (config C5) instead of one
+    diffusion, with per-step sums; dump then holds attribute 0."""
     import json
     if not os.path.exists(CPU_MPI_PATH):
         subprocess.run(["make", "-s", "-C", HERE, "cpu_mpi"], check=True)
@@ -44,7 +46,11 @@ def cpu_mpi(H, W, rate, seconds, ranks, maxsteps=100000, dump=None, timeout=600)
            str(H), str(W), repr(float(rate)), repr(float(seconds)), str(maxsteps)]
     if dump:
         cmd.append(dump)
-    r = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ)
+    env.pop("MM_PROGRAM", None)
+    if program:
+        env["MM_PROGRAM"] = ",".join(f"{k}:{a}:{b}:{float(r)!r}" for k, a, b, r in program)
+    r = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout, env=env)
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 

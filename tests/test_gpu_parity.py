@@ -168,10 +168,9 @@ def make_env_engine(gpu, monkeypatch, H, W, n_attr=1, **env):
     return e
 
 
-# every way the engine can run a single-diffusion program: one step per pass, the
-# two-step pair kernel, and the K-step overlapped-strip kernel at each K / row block /
-# block order
-FUSE_ENVS = [{"MM_FUSE": 0}, {"MM_PASSK": 0}, {"MM_PASSK": 0, "MM_ROWS_PER_WAVE2": 8}, {}] + [
+# every way the engine can run a single-diffusion program: one step per pass, and the
+# K-step overlapped-strip kernel at each K / row block / block order
+FUSE_ENVS = [{"MM_PASSK": 0}, {}] + [
     {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3)
 ] + [{"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0},
      {"MM_XCD_REMAP": 1}, {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16}]
@@ -242,7 +241,11 @@ def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k):
     e.run(steps, 3)
     got = e.download()
     hist = e.sums_history()
+    info = e.info()
     e.close()
+    # the steps really were replayed as hipGraphs (a refused capture would run eagerly)
+    assert info["graph_state"] == 1 and info["graph_launches"] >= 1, info
+    assert info["hist_entries"] == steps // 3
     ref = O.fill_random(H, W)
     sums = []
     for s in range(1, steps + 1):
@@ -358,7 +361,7 @@ def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     steps = 2 * depth  # two passes: afterwards the current buffer's ghost rows hold the
                        # rows exchanged in the first pass (the initial state's)
     env = {"MM_SELF_HALO": 1, "MM_GRAPH": graph}
-    env.update({"MM_FUSE": 0} if k == 1 else {"MM_STEPS_PER_PASS": k})
+    env.update({"MM_PASSK": 0} if k == 1 else {"MM_STEPS_PER_PASS": k})
     for key, v in env.items():
         monkeypatch.setenv(key, str(v))
     e = gpu.Engine(H, W, halo_mode=gpu.MM_HALO_RCCL, comm_id_bytes=gpu.comm_id())
@@ -373,7 +376,13 @@ def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     top = e.read_rows(-depth, depth)
     bot = e.read_rows(H, depth)
     hist = e.sums_history()
+    info = e.info()
     e.close()
+    # graph=1: the RCCL calls were captured and replayed, not silently run eagerly
+    if graph:
+        assert info["graph_state"] == 1 and info["graph_launches"] == 1, info
+    else:
+        assert info["graph_state"] == 0 and info["graph_launches"] == 0, info
     ref = v0
     sums = []
     for _ in range(steps):

@@ -129,6 +129,28 @@ def test_cpu_mpi_baseline_is_the_oracle(O, tmp_path, H, W, P, steps):
     assert np.array_equal(got, want)
 
 
+C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
+            (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+
+
+@pytest.mark.parametrize("H,W,P,steps", [(37, 29, 3, 4), (16, 130, 4, 3)])
+def test_cpu_mpi_program_baseline_is_the_oracle(O, tmp_path, H, W, P, steps):
+    """The MPI CPU baseline's flow-program mode (config C5: 4 attributes, chained
+    transfers + diffusions, per-step sums) reproduces or_program_step bit for bit."""
+    if not os.path.exists(os.path.join(O.MPI_HOME, "bin", "mpirun")):
+        pytest.skip("no MPI")
+    out = tmp_path / "grid.bin"
+    r = O.cpu_mpi(H, W, 0.1, 0, P, maxsteps=-steps, dump=str(out), timeout=120,
+                  program=C5_FLOWS)
+    assert r["ranks"] == P and r["steps"] == steps and r["n_attr"] == 4 and r["n_flows"] == 8
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    want = O.program_step(fields, C5_FLOWS, steps=steps)
+    got = np.fromfile(out, dtype=np.float64).reshape(H, W)
+    assert np.array_equal(got, want[0])
+    total = math.fsum(np.concatenate([f.ravel() for f in want]))
+    assert abs(r["total"] - total) <= 1e-12 * total
+
+
 def test_program_step_conserves_total(O):
     H, W = 24, 40
     fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
