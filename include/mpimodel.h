@@ -117,6 +117,41 @@ int mm_partition_rows(long long H, int G, int g, long long* x_init, long long* h
 /* src/Cell.hpp:71-157 -- Moore neighbour count of (x,y): 3 corner, 5 edge, 8 inside. */
 int mm_neighbor_count(long long H, long long W, long long x, long long y);
 
+/* src/ModelRectangular.hpp:69-80 -- 2-D block descriptor of worker k (1-based) of the
+ * block model: blocks of (H/lines) x (W/columns) cells dealt row-major; the column
+ * offset wraps to the next band of rows only when it lands exactly on W (int
+ * arithmetic as the reference, which never wraps when columns does not divide W). */
+int mm_partition_rect_reference(int H, int W, int lines, int columns, int k,
+                                int* x_init, int* y_init, int* height, int* width);
+/* src/ModelRectangular.hpp:85 -- owner rank of the source (x,y): (x+y)/space_height + 1
+ * (the reference's formula, bug included). */
+int mm_owner_rect_reference(int space_height, int x, int y);
+
+/* src/Model.hpp:176-235 -- does the reference's single-source flow change any cell when
+ * run by P workers? 1 only for a source with 8 neighbours on the last row of its owner's
+ * slab (src/Model.hpp:189-216) whose owner has a successor (the share of the row below
+ * goes to owner+1, :202-204); 0 otherwise (the reference does nothing there -- and its
+ * owner+1 then waits forever, or it aborts); -1 for bad arguments. */
+int mm_point_strict_applies(int H, int W, int P, int x, int y);
+
+/* Control-message wire format (src/Model.hpp:70-86,138-167,
+ * src/ModelRectangular.hpp:69-92): the master sends every worker a MM_WIRE_LEN-char
+ * partition descriptor "%d|%d:%d|%d" = x_init|y_init:height|width (tag 0, FROM_MASTER)
+ * and a flow descriptor "%d|%d:%d|%lf" = owner|x:y|rate (tag 999). Formatting writes
+ * the text, NUL-padded to len (MM_ERR_INVALID if it does not fit; the reference's
+ * sprintf would overflow its buffer). Parsing follows the reference's strtok/atoi
+ * sequence; for the flow it also returns the rate as the reference reads it (atoi, an
+ * int) and losslessly (strtod). */
+#define MM_WIRE_LEN 23
+#define MM_TAG_PARTITION 0
+#define MM_TAG_FLOW 999
+int mm_wire_format_partition(char* out, int len, int x_init, int y_init, int height, int width);
+int mm_wire_format_flow(char* out, int len, int owner, int x, int y, double rate);
+int mm_wire_parse_partition(const char* msg, int len, int* x_init, int* y_init, int* height,
+                            int* width);
+int mm_wire_parse_flow(const char* msg, int len, int* owner, int* x, int* y, int* rate_atoi,
+                       double* rate);
+
 /* RCCL bootstrap: rank 0 creates the id, every rank passes it in mm_desc.comm_id.
  * Replaces the master's partition/flow descriptor messages (src/Model.hpp:70-86). */
 int mm_comm_id_size(void);
@@ -160,6 +195,11 @@ int mm_add_flow(mm_engine* eng, int kind, int a, int b, double rate);
  * (every slab computes the share from the same flow description). */
 int mm_point_apply(mm_engine* eng, int attr, long long sx, long long sy,
                    double captured, double rate);
+/* Strict-reference point mode (opt-in): the same update, applied only where the
+ * reference's P-worker run applies it (mm_point_strict_applies); elsewhere the grid is
+ * left unchanged, as the reference leaves it. *applied (may be NULL) reports which. */
+int mm_point_apply_strict(mm_engine* eng, int attr, long long sx, long long sy,
+                          double captured, double rate, int P, int* applied);
 
 /* Run nsteps steps of the flow program (the commented-out time loop,
  * src/Model.hpp:180-183, made real). Every reduce_every-th step (0 = never; steps

@@ -2,8 +2,8 @@
 // (reference: src/CellularSpace.hpp:8-34). The reference embeds a static
 // Cell[PROC_DIMX*PROC_DIMY] array (96 B per cell, on the stack); here the space is a
 // descriptor and the cell values live on the GPU as fp64 arrays owned by the engine
-// (Model::execute). `memoria` is filled only by Model::execute's result download
-// when the caller asks for it (MM_KEEP_RESULT=1), so memory stays O(1) by default.
+// (Model::execute). `memoria` stays empty: results reach the caller as the reference's
+// output files and through MPI_Report, so host memory stays O(1).
 #ifndef CELLULARSPACE_HPP
 #define CELLULARSPACE_HPP
 

@@ -1,10 +1,14 @@
 // ModelRectangular.hpp -- the 2-D block variant of Model
-// (reference: src/ModelRectangular.hpp:13-273). The reference cuts a DIMX_REC x DIMY_REC
-// grid into LINES_REC x COLUMNS_REC blocks (:69-80) but changes no cell (its owner and
-// index arithmetic miss the source). Here the block descriptors are
-// computed with the same integer bookkeeping (rect_block) and the flow itself is run
-// by the row-slab engine, which is the better decomposition on one node of GPUs
-// (contiguous border rows, one exchange partner per side).
+// (reference: src/ModelRectangular.hpp:13-273). The reference cuts the DIMX_REC x DIMY_REC
+// grid of DefinesRectangular.hpp into LINES_REC x COLUMNS_REC blocks, sends each worker its
+// block descriptor and the flow descriptor (:69-92), but changes no cell (its owner and
+// index arithmetic miss the source) and writes no result (:94-129,236-270
+// are commented out). Here the master sends the same descriptors (mm_partition_rect_reference,
+// mm_owner_rect_reference, mm_wire_*: byte-identical to the reference's,
+// tests/golden/wire_rect_*.json) and reports them in MPI_Report::blocks / owner; the flow
+// itself is run on the grid by the row-slab engine (the better decomposition on one node of
+// GPUs: contiguous border rows, one exchange partner per side). As the reference, no
+// result files are written unless MM_WRITE_OUTPUT=1.
 #ifndef MODELRECTANGULAR_HPP
 #define MODELRECTANGULAR_HPP
 
@@ -14,25 +18,6 @@
 #include "MPIImpl.hpp"
 #include "MPI_Report.hpp"
 #include "mm_driver.hpp"
-
-namespace mm {
-// src/ModelRectangular.hpp:69-80: descriptor of worker k (1-based): blocks are dealt
-// row-major, PROC_DIMY_REC columns at a time, wrapping to the next band of rows.
-inline void rect_block(int k, int* x_init, int* y_init, int* height, int* width) {
-    int ox = 0, oy = 0;
-    for (int dest = 1; dest < k; ++dest) {
-        oy += PROC_DIMY_REC;
-        if (oy == DIMY_REC) {
-            ox += PROC_DIMX_REC;
-            oy = 0;
-        }
-    }
-    *x_init = ox;
-    *y_init = oy;
-    *height = PROC_DIMX_REC;
-    *width = PROC_DIMY_REC;
-}
-}  // namespace mm
 
 template <class T>
 class ModelRectangular {
@@ -71,9 +56,13 @@ public:
         f.captured = flow.source.attribute.value;
         f.rate = flow.flow_rate;
         f.attribute = flow.attribute;
-        if (!f.whole_grid) flow.last_execute = flow.execute();
-        mm::run_model<R>(mpi_comm, f, time, time_step, cellular_space.height,
-                         cellular_space.width, report);
+        if (!f.whole_grid) flow.last_execute = flow.execute();  // src/ModelRectangular.hpp:179
+        mm::Layout L;
+        L.rect = true;
+        L.lines = LINES_REC;
+        L.columns = COLUMNS_REC;
+        L.space_height = cellular_space.height;  // the owner formula's divisor (:85)
+        mm::run_model<R>(mpi_comm, f, time, time_step, DIMX_REC, DIMY_REC, report, L);
     }
 };
 

@@ -1,21 +1,35 @@
-// mm_driver.hpp -- the MPI master/worker driver behind Model::execute (drop-in API).
+// mm_driver.hpp -- the MPI master/worker driver behind Model::execute and
+// ModelRectangular::execute (drop-in API).
 //
-// Keeps the reference's process layout (src/Model.hpp:53-262): rank 0 is the master
-// (no cells: it reduces the workers' sums, checks conservation, merges the result
-// files), ranks 1..P are workers, each owning one row slab. What changed is what a
-// worker is: a GPU engine (include/mpimodel.h) instead of a stack array of 96-B cells.
-//   * partition descriptors and the flow descriptor are computed on every rank
-//     (identical integer bookkeeping, src/Model.hpp:60-86) instead of being sent as
-//     23-char strings;
+// Keeps the reference's process layout and control plane (src/Model.hpp:53-262,
+// src/ModelRectangular.hpp:52-272): rank 0 is the master (no cells), ranks 1..P are
+// workers. The master sends every worker the reference's 23-char partition descriptor
+// ("%d|%d:%d|%d", tag 0) and flow descriptor ("%d|%d:%d|%lf", tag 999) -- the same bytes
+// (tests/golden/wire_*.json), formatted and parsed by the C ABI (mm_wire_*); it then
+// reduces the workers' sums in rank order, checks conservation and merges the result
+// files. What changed is what a worker is: a GPU engine (include/mpimodel.h) instead of
+// a stack array of 96-B cells.
+//   * Model: row slabs. A worker owns rows mm_partition_rows(H, P, k-1), which are the
+//     descriptor's rows whenever P divides H (the only layout the reference itself
+//     completes); when it does not, the reference drops the
+//     remainder rows while the engine slabs cover them.
+//   * ModelRectangular: the DIMX_REC x DIMY_REC grid of DefinesRectangular.hpp, 2-D block
+//     descriptors (mm_partition_rect_reference) and owner formula (mm_owner_rect_reference)
+//     as the reference; the cells are computed on row slabs (the better decomposition for
+//     GPUs on one node), and, as the reference, no result files by default.
 //   * the single-source flow (reference form) is applied by every slab to the cells it
 //     owns, so the scalar halo messages src/Model.hpp:202-204 / :228-230 disappear;
 //   * a whole-grid flow (Exponencial(rate)) runs step_count(time, time_step) steps
 //     (the commented-out loop, src/Model.hpp:180-183) with border rows exchanged over
-//     RCCL (workers on distinct GPUs) or through MPI (workers sharing a GPU);
+//     RCCL (workers on distinct GPUs) or through MPI (workers sharing a GPU: halo_depth
+//     rows per exchange, then halo_depth steps on the device);
 //   * the per-rank text dump and the master's merge keep the reference's format
 //     (src/Model.hpp:97-131,245-260).
 // Environment: MM_OUTPUT_DIR (default "../output", as the reference),
-//              MM_WRITE_OUTPUT=0 disables the text files (large grids).
+//              MM_WRITE_OUTPUT=0/1 disables / enables the text files (large grids),
+//              MM_STRICT_REFERENCE=1 applies a single-source flow only where the
+//              reference's P-worker run does (mm_point_apply_strict; elsewhere, e.g. an
+//              edge source, the grid is left as the reference leaves it).
 #ifndef MM_DRIVER_HPP
 #define MM_DRIVER_HPP
 
@@ -44,14 +58,22 @@ struct FlowSpec {
     int attribute;
 };
 
+// Which reference model drives the run.
+struct Layout {
+    bool rect = false;      // ModelRectangular: 2-D block descriptors
+    int lines = 1, columns = 1;
+    int space_height = 0;   // the caller's space height (ModelRectangular owner formula)
+};
+
 inline std::string output_dir() {
     const char* d = std::getenv("MM_OUTPUT_DIR");
     return d ? std::string(d) : std::string("../output");
 }
 
-inline bool write_output() {
+inline bool write_output(bool dflt) {
     const char* w = std::getenv("MM_WRITE_OUTPUT");
-    return !(w && std::strcmp(w, "0") == 0);
+    if (!w) return dflt;
+    return std::strcmp(w, "0") != 0;
 }
 
 // Workers' communicator and device placement.
@@ -82,20 +104,21 @@ inline WorkerComm make_worker_comm(const MPI_Comm& comm, bool is_worker) {
     return w;
 }
 
-// One step of the MPI host transport: first/last owned rows to the neighbours,
-// their rows into the ghost rows (whole rows; replaces src/Model.hpp:202-204,228-230).
-inline void host_halo(Engine& e, const WorkerComm& w, std::vector<double>& top,
+// One exchange of the MPI host transport: the first / last `rows` owned rows to the
+// neighbours, theirs into the ghost rows (whole rows, `rows` deep; replaces
+// src/Model.hpp:202-204,228-230).
+inline void host_halo(Engine& e, const WorkerComm& w, int rows, std::vector<double>& top,
                       std::vector<double>& bot, std::vector<double>& gtop,
                       std::vector<double>& gbot) {
     const int up = w.wrank > 0 ? w.wrank - 1 : MPI_PROC_NULL;
     const int down = w.wrank < w.wsize - 1 ? w.wrank + 1 : MPI_PROC_NULL;
-    const int n = (int)top.size();
-    e.halo_export(top.data(), bot.data());
+    const int n = (int)(rows * e.desc().W);
+    e.halo_export(rows, top.data(), bot.data());
     MPI_Sendrecv(top.data(), n, MPI_DOUBLE, up, 71, gbot.data(), n, MPI_DOUBLE, down, 71,
                  w.wcomm, MPI_STATUS_IGNORE);
     MPI_Sendrecv(bot.data(), n, MPI_DOUBLE, down, 72, gtop.data(), n, MPI_DOUBLE, up, 72,
                  w.wcomm, MPI_STATUS_IGNORE);
-    e.halo_import(up == MPI_PROC_NULL ? nullptr : gtop.data(),
+    e.halo_import(rows, up == MPI_PROC_NULL ? nullptr : gtop.data(),
                   down == MPI_PROC_NULL ? nullptr : gbot.data());
 }
 
@@ -129,10 +152,37 @@ inline void merge_files(const std::vector<std::string>& names) {
     }
 }
 
+// The control messages of worker k (1-based): what the reference's master sends.
+struct Descriptors {
+    char partition[MM_WIRE_LEN];
+    char flow[MM_WIRE_LEN];
+    int owner;
+};
+
+inline Descriptors make_descriptors(const Layout& L, const FlowSpec& f, int H, int W, int P,
+                                    int k) {
+    Descriptors d;
+    int x0, y0, h, w;
+    if (L.rect)
+        check(mm_partition_rect_reference(H, W, L.lines, L.columns, k, &x0, &y0, &h, &w));
+    else
+        check(mm_partition_reference(H, W, P, k, &x0, &y0, &h, &w));
+    check(mm_wire_format_partition(d.partition, MM_WIRE_LEN, x0, y0, h, w));
+    if (f.whole_grid) {  // extension: every cell is a source; no owner, no source cell
+        d.owner = 0;
+        check(mm_wire_format_flow(d.flow, MM_WIRE_LEN, 0, -1, -1, f.rate));
+    } else {
+        d.owner = L.rect ? mm_owner_rect_reference(L.space_height, (int)f.src_x, (int)f.src_y)
+                         : mm_owner_reference(H, P, (int)f.src_x);
+        check(mm_wire_format_flow(d.flow, MM_WIRE_LEN, d.owner, (int)f.src_x, (int)f.src_y, f.rate));
+    }
+    return d;
+}
+
 // The worker body: one slab on one GPU. Returns the slab sum (src/Model.hpp:237-240).
 template <class R>
-double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, double time,
-              double time_step, long long H, long long W, std::vector<double>& hist,
+double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, int owner, double time,
+              double time_step, long long H, long long W, bool files, std::vector<double>& hist,
               double& seconds, int& halo_mode, std::string& file) {
     mm_desc d;
     std::memset(&d, 0, sizeof d);
@@ -158,13 +208,18 @@ double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, double ti
     seconds = 0.0;
     if (!f.whole_grid) {
         // src/Model.hpp:176-182: the owner reports the source cell and the outflow
-        const int owner = mm_owner_reference((int)H, P, (int)f.src_x);
         if (rank == owner) {
             std::cout << f.src_x << " " << f.src_y << " "
                       << mm_neighbor_count(H, W, f.src_x, f.src_y) << std::endl;
             std::cout << rank << ": " << f.rate * f.captured << std::endl;
         }
-        e.point_apply(0, f.src_x, f.src_y, f.captured, f.rate);
+        const char* strict = std::getenv("MM_STRICT_REFERENCE");
+        if (f.src_x < H && f.src_y < W) {
+            if (strict && std::strcmp(strict, "0") != 0)
+                e.point_apply_strict(0, f.src_x, f.src_y, f.captured, f.rate, P);
+            else
+                e.point_apply(0, f.src_x, f.src_y, f.captured, f.rate);
+        }
         e.synchronize();
     } else {
         e.add_flow(MM_FLOW_DIFFUSE, 0, 0, f.rate);
@@ -172,10 +227,16 @@ double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, double ti
         MPI_Barrier(w.wcomm);
         const auto t0 = std::chrono::steady_clock::now();
         if (d.halo_mode == MM_HALO_HOST) {
-            std::vector<double> top((size_t)W), bot((size_t)W), gtop((size_t)W), gbot((size_t)W);
-            for (long long s = 0; s < n; ++s) {
-                host_halo(e, w, top, bot, gtop, gbot);
-                e.run(1, 1);
+            // workers sharing a GPU: halo_depth rows per MPI exchange, then as many steps
+            // in one K-step kernel pass
+            const int depth = e.info().halo_depth;
+            const size_t sz = (size_t)depth * (size_t)W;
+            std::vector<double> top(sz), bot(sz), gtop(sz), gbot(sz);
+            for (long long s = 0; s < n;) {
+                const int k = (int)std::min<long long>(depth, n - s);
+                host_halo(e, w, k, top, bot, gtop, gbot);
+                e.run(k, 1);
+                s += k;
             }
         } else {
             e.run(n, 1);
@@ -185,7 +246,7 @@ double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, double ti
         hist = e.history();
     }
     const double local = e.sums()[0];
-    if (write_output()) {
+    if (files) {
         std::vector<double> v = e.download(0);
         file = write_rank_file<R>(rank, d.x_init, d.h, W, v);
     }
@@ -194,23 +255,53 @@ double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, double ti
 
 template <class R>
 void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time_step,
-               long long H, long long W, MPI_Report& rep) {
+               long long H, long long W, MPI_Report& rep, const Layout& L = Layout()) {
     int size = 1, rank = 0;
     MPI_Comm_size(comm, &size);
     MPI_Comm_rank(comm, &rank);
     const bool single = size == 1;  // one process: master and the only worker
     const int P = single ? 1 : size - 1;
+    const bool files = write_output(!L.rect);  // ModelRectangular writes none (as the reference)
     rep.comm_size = size;
     rep.rank_id = rank;
     rep.initial_sum = (double)H * (double)W;  // every cell starts at 1.0
 
-    if (rank == 0 && !f.whole_grid) {
-        // src/Model.hpp:80-82: the flow descriptor line the reference master prints
-        char line[64];
-        std::snprintf(line, sizeof line, "%d|%lld:%lld|%lf", mm_owner_reference((int)H, P, (int)f.src_x),
-                      f.src_x, f.src_y, f.rate);
-        std::cout << line << std::endl;
+    // control plane: the reference's descriptors, master -> every worker
+    Descriptors mine = make_descriptors(L, f, (int)H, (int)W, P, single ? 1 : (rank ? rank : 1));
+    rep.owner = mine.owner;
+    if (rank == 0) {
+        rep.blocks.clear();
+        for (int k = 1; k <= P; ++k) {
+            const Descriptors dk = make_descriptors(L, f, (int)H, (int)W, P, k);
+            int x0, y0, h, w;
+            check(mm_wire_parse_partition(dk.partition, MM_WIRE_LEN, &x0, &y0, &h, &w));
+            rep.blocks.insert(rep.blocks.end(), {x0, y0, h, w});
+            if (!single) MPI_Send(dk.partition, MM_WIRE_LEN, MPI_CHAR, k, MM_TAG_PARTITION, comm);
+        }
+        if (!f.whole_grid) {
+            // src/Model.hpp:82 (ModelRectangular.hpp:88 appends the owner)
+            if (L.rect)
+                std::cout << mine.flow << " " << mine.owner << std::endl;
+            else
+                std::cout << mine.flow << std::endl;
+        }
+        if (!single)
+            for (int k = 1; k <= P; ++k)
+                MPI_Send(mine.flow, MM_WIRE_LEN, MPI_CHAR, k, MM_TAG_FLOW, comm);
     }
+    int owner = mine.owner;
+    if (!single && rank != 0) {
+        // src/Model.hpp:138-167: the worker's receive and strtok/atoi parse
+        char part[MM_WIRE_LEN + 1] = {0}, flow[MM_WIRE_LEN + 1] = {0};
+        MPI_Recv(part, MM_WIRE_LEN, MPI_CHAR, 0, MM_TAG_PARTITION, comm, MPI_STATUS_IGNORE);
+        MPI_Recv(flow, MM_WIRE_LEN, MPI_CHAR, 0, MM_TAG_FLOW, comm, MPI_STATUS_IGNORE);
+        int x0, y0, h, w, fx, fy, rate_atoi;
+        double rate;
+        check(mm_wire_parse_partition(part, MM_WIRE_LEN, &x0, &y0, &h, &w));
+        check(mm_wire_parse_flow(flow, MM_WIRE_LEN, &owner, &fx, &fy, &rate_atoi, &rate));
+        if (L.rect) std::cout << flow << std::endl;  // src/ModelRectangular.hpp:158
+    }
+
     const bool is_worker = single || rank != 0;
     WorkerComm w = make_worker_comm(comm, is_worker);
     std::vector<double> hist;
@@ -218,8 +309,8 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
     int halo_mode = 0;
     std::string file;
     if (is_worker)
-        local = worker<R>(w, single ? 1 : rank, P, f, time, time_step, H, W, hist, seconds,
-                          halo_mode, file);
+        local = worker<R>(w, single ? 1 : rank, P, f, owner, time, time_step, H, W, files, hist,
+                          seconds, halo_mode, file);
 
     long long n = f.whole_grid ? mm_step_count(time, time_step) : 0;
     if (single) {
@@ -229,8 +320,9 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         rep.devices = 1;
         rep.steps = n;
         rep.gcups = seconds > 0 ? (double)H * W * n / seconds / 1e9 : 0.0;
+        rep.final_sum = local;
         assert(std::fabs(local - rep.initial_sum) <= 1e-9 * rep.initial_sum);
-        if (write_output()) merge_files(std::vector<std::string>(1, file));
+        if (files) merge_files(std::vector<std::string>(1, file));
     } else if (rank == 0) {
         // src/Model.hpp:88-95: per-worker sums, received in rank order
         double acc = 0.0;
@@ -253,12 +345,15 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         rep.steps = n;
         rep.gcups = rep.seconds > 0 ? (double)H * W * n / rep.seconds / 1e9 : 0.0;
         // the reference's check, made two-sided and size-aware (src/Model.hpp:95)
+        rep.final_sum = acc;
         assert(std::fabs(acc - rep.initial_sum) <= 1e-9 * rep.initial_sum);
-        if (write_output()) {
+        if (files) {
+            // src/Model.hpp:110-111: file names in rank order, tag = rank
             std::vector<std::string> names;
             for (int k = 1; k <= P; ++k) {
                 char buf[512];
-                MPI_Recv(buf, (int)sizeof buf, MPI_CHAR, k, 4000 + k, comm, MPI_STATUS_IGNORE);
+                std::memset(buf, 0, sizeof buf);
+                MPI_Recv(buf, (int)sizeof buf - 1, MPI_CHAR, k, k, comm, MPI_STATUS_IGNORE);
                 names.push_back(std::string(buf));
             }
             merge_files(names);
@@ -275,11 +370,13 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
             MPI_Send(&devs, 1, MPI_INT, 0, 3001, comm);
             MPI_Send(&halo_mode, 1, MPI_INT, 0, 3002, comm);
         }
-        if (write_output()) {
+        if (files) {
+            // src/Model.hpp:260: the file name, 30 chars as the reference when it fits
             char buf[512];
             std::memset(buf, 0, sizeof buf);
             std::strncpy(buf, file.c_str(), sizeof buf - 1);
-            MPI_Send(buf, (int)sizeof buf, MPI_CHAR, 0, 4000 + rank, comm);  // src/Model.hpp:260
+            const int len = file.size() < 30 ? 30 : (int)file.size() + 1;
+            MPI_Send(buf, len, MPI_CHAR, 0, rank, comm);
         }
     }
     if (w.wcomm != MPI_COMM_NULL) MPI_Comm_free(&w.wcomm);

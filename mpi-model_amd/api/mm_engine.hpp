@@ -4,6 +4,7 @@
 #ifndef MM_ENGINE_HPP
 #define MM_ENGINE_HPP
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -32,6 +33,12 @@ public:
     void point_apply(int attr, long long sx, long long sy, double captured, double rate) {
         check(mm_point_apply(e_, attr, sx, sy, captured, rate));
     }
+    bool point_apply_strict(int attr, long long sx, long long sy, double captured, double rate,
+                            int workers) {
+        int applied = 0;
+        check(mm_point_apply_strict(e_, attr, sx, sy, captured, rate, workers, &applied));
+        return applied != 0;
+    }
     void run(long long steps, long long reduce_every) { check(mm_run(e_, steps, reduce_every)); }
     void synchronize() { check(mm_synchronize(e_)); }
     std::vector<double> sums() {
@@ -43,7 +50,9 @@ public:
         long long n = 0;
         check(mm_sums_history(e_, nullptr, 0, &n));
         std::vector<double> h((size_t)n * d_.n_attr);
-        if (n) check(mm_sums_history(e_, h.data(), n, &n));
+        long long got = n;
+        if (n) check(mm_sums_history(e_, h.data(), n, &got));
+        h.resize((size_t)std::min(n, got) * d_.n_attr);
         return h;
     }
     std::vector<double> download(int attr) {
@@ -51,9 +60,17 @@ public:
         check(mm_download(e_, attr, v.data()));
         return v;
     }
-    void halo_export(double* top, double* bottom) { check(mm_halo_export(e_, top, bottom)); }
-    void halo_import(const double* top, const double* bottom) {
-        check(mm_halo_import(e_, top, bottom));
+    mm_info info() {
+        mm_info i;
+        check(mm_engine_info(e_, &i));
+        return i;
+    }
+    // first / last nrows owned rows of every attribute, [attr][row][col]
+    void halo_export(int nrows, double* top, double* bottom) {
+        check(mm_halo_export_rows(e_, nrows, top, bottom));
+    }
+    void halo_import(int nrows, const double* top, const double* bottom) {
+        check(mm_halo_import_rows(e_, nrows, top, bottom));
     }
 
 private:

@@ -100,7 +100,7 @@ struct mm_engine {
 
     int th = 8;              // rows per wave, one-step kernel
     bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
-    int kpass = 4;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps)
+    int kpass = 7;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
     double seg_waves = 2.0;  // segment waves per resident wave slot (MM_SEG_WAVES)
     double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
@@ -832,6 +832,7 @@ int mm_engine_destroy(mm_engine* e) {
     if (e->hist) (void)hipFree(e->hist);
     if (e->hist_n) (void)hipFree(e->hist_n);
     if (e->sum_tmp) (void)hipFree(e->sum_tmp);
+    (void)hipGetLastError();  // statuses above are ignored on purpose; do not leave them pending
     delete e;
     return MM_OK;
 }
@@ -943,6 +944,18 @@ int mm_point_apply(mm_engine* e, int attr, long long sx, long long sy, double ca
     MM_HIP(mm::launch_point(e->buf[e->cur][attr], e->pitch, e->d.H, e->d.W, e->d.x_init, e->d.h,
                             sx, sy, captured, rate, e->s_comp));
     return MM_OK;
+}
+
+int mm_point_apply_strict(mm_engine* e, int attr, long long sx, long long sy, double captured,
+                          double rate, int P, int* applied) {
+    if (applied) *applied = 0;
+    if (!e || e->d.H > INT32_MAX || e->d.W > INT32_MAX)
+        return fail(MM_ERR_INVALID, "mm_point_apply_strict: bad arguments");
+    const int ok = mm_point_strict_applies((int)e->d.H, (int)e->d.W, P, (int)sx, (int)sy);
+    if (ok < 0) return fail(MM_ERR_INVALID, "mm_point_apply_strict: bad source or worker count");
+    if (ok == 0) return MM_OK;  // the reference changes no cell here
+    if (applied) *applied = 1;
+    return mm_point_apply(e, attr, sx, sy, captured, rate);
 }
 
 int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {

@@ -47,9 +47,26 @@ __device__ __forceinline__ int span3(long long n, long long i) {
     return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
 }
 
-// share of one emitter (src/Model.hpp:199); cnt == 8 as the exact *0.125
+// share of one emitter of the reference's single-source flow (src/Model.hpp:199); cnt ==
+// 8 as the exact *0.125
 __device__ __forceinline__ double share_of(double out, int cnt) {
     return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
+}
+
+// One emitter of the whole-grid step (oracle/mm_oracle.c emit): share s and kept value
+// d = u - out; cnt == 8 as s = u*(r/8), d = fma(s, -8, u).
+__device__ __forceinline__ void emit_one(double r, double u, int cnt, double& s, double& d) {
+    if (cnt == 8) {
+        s = u * (r * 0.125);
+        d = __builtin_fma(s, -8.0, u);
+    } else if (cnt > 0) {
+        const double out = r * u;
+        s = out / (double)cnt;
+        d = u - out;
+    } else {
+        s = 0.0;
+        d = u;
+    }
 }
 
 // Chain entries are read with compile-time indices only, so they are scalar loads of
@@ -155,13 +172,12 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             if (A.diffuse_mask & (1 << a)) {
-                const double r_ = A.drate[a];
-                const double o0 = r_ * u0[a], o1 = r_ * u1[a], oe = r_ * ue[a];
-                o.s0[a] = o0 * 0.125;
-                o.s1[a] = o1 * 0.125;
-                o.se[a] = oe * 0.125;
-                o.d0[a] = u0[a] - o0;
-                o.d1[a] = u1[a] - o1;
+                const double r8 = A.drate[a] * 0.125;
+                o.s0[a] = u0[a] * r8;
+                o.s1[a] = u1[a] * r8;
+                o.se[a] = ue[a] * r8;
+                o.d0[a] = __builtin_fma(o.s0[a], -8.0, u0[a]);
+                o.d1[a] = __builtin_fma(o.s1[a], -8.0, u1[a]);
             } else {
                 o.s0[a] = o.s1[a] = o.se[a] = 0.0;
                 o.d0[a] = u0[a];
@@ -177,14 +193,10 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
     for (int a = 0; a < NA; ++a) {
         if (A.diffuse_mask & (1 << a)) {
             const double r_ = A.drate[a];
-            const double o0 = c0 > 0 ? r_ * u0[a] : 0.0;
-            const double o1 = c1 > 0 ? r_ * u1[a] : 0.0;
-            const double oe = ce > 0 ? r_ * ue[a] : 0.0;
-            o.s0[a] = share_of(o0, c0);
-            o.s1[a] = share_of(o1, c1);
-            o.se[a] = share_of(oe, ce);
-            o.d0[a] = u0[a] - o0;
-            o.d1[a] = u1[a] - o1;
+            double de;
+            emit_one(r_, u0[a], c0, o.s0[a], o.d0[a]);
+            emit_one(r_, u1[a], c1, o.s1[a], o.d1[a]);
+            emit_one(r_, ue[a], ce, o.se[a], de);
         } else {
             o.s0[a] = o.s1[a] = o.se[a] = 0.0;
             o.d0[a] = u0[a];

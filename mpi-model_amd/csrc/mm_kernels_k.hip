@@ -63,6 +63,10 @@ int passk_waves_per_cu(int k, int na, bool red, int nt) {
         case 2: return passk_waves_k2(na, red, nt);
         case 3: return passk_waves_k3(na, red, nt);
         case 4: return passk_waves_k4(na, red, nt);
+        case 5: return passk_waves_k5(na, red, nt);
+        case 6: return passk_waves_k6(na, red, nt);
+        case 7: return passk_waves_k7(na, red, nt);
+        case 8: return passk_waves_k8(na, red, nt);
         default: return 0;
     }
 }
@@ -74,6 +78,10 @@ hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t 
         case 2: return passk_launch_k2(na, red, a, s, variant);
         case 3: return passk_launch_k3(na, red, a, s, variant);
         case 4: return passk_launch_k4(na, red, a, s, variant);
+        case 5: return passk_launch_k5(na, red, a, s, variant);
+        case 6: return passk_launch_k6(na, red, a, s, variant);
+        case 7: return passk_launch_k7(na, red, a, s, variant);
+        case 8: return passk_launch_k8(na, red, a, s, variant);
         default: return hipErrorInvalidValue;
     }
 }

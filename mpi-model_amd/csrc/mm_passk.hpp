@@ -37,8 +37,9 @@
 //   * BLOCK: 4 rows, fully unrolled -- the border rows of a halo-split pass.
 //
 // Every level uses exactly the single-step arithmetic of oracle/mm_oracle.h (transfers
-// in declared order, then out = r*u, s = out/cnt, v' = (u - out) + nb), so K fused steps
-// are bit-identical to K single steps (built with -ffp-contract=off).
+// in declared order, then per emitter s = out/cnt and d = u - out -- for cnt == 8 as
+// s = u*(r/8), d = fma(s, -8, u) -- and v' = d + nb), so K fused steps are bit-identical
+// to K single steps (built with -ffp-contract=off; the one fma is explicit).
 //
 // This header holds the kernel templates; mm_passk_k<K>.hip instantiate them (one
 // translation unit per K so the builds run in parallel) and mm_kernels_k.hip dispatches.
@@ -48,16 +49,20 @@
 
 namespace mm {
 
-// per-K entry points (mm_passk_k1.hip .. mm_passk_k4.hip); na outside the TU's set is
+// per-K entry points (mm_passk_k1.hip .. mm_passk_k8.hip); na outside the TU's set is
 // hipErrorInvalidValue / 0
-hipError_t passk_launch_k1(int na, bool red, const PassArgs& a, hipStream_t s, int v);
-hipError_t passk_launch_k2(int na, bool red, const PassArgs& a, hipStream_t s, int v);
-hipError_t passk_launch_k3(int na, bool red, const PassArgs& a, hipStream_t s, int v);
-hipError_t passk_launch_k4(int na, bool red, const PassArgs& a, hipStream_t s, int v);
-int passk_waves_k1(int na, bool red, int nt);
-int passk_waves_k2(int na, bool red, int nt);
-int passk_waves_k3(int na, bool red, int nt);
-int passk_waves_k4(int na, bool red, int nt);
+#define MM_PASSK_DECL(K)                                                                  \
+    hipError_t passk_launch_k##K(int na, bool red, const PassArgs& a, hipStream_t s, int v); \
+    int passk_waves_k##K(int na, bool red, int nt);
+MM_PASSK_DECL(1)
+MM_PASSK_DECL(2)
+MM_PASSK_DECL(3)
+MM_PASSK_DECL(4)
+MM_PASSK_DECL(5)
+MM_PASSK_DECL(6)
+MM_PASSK_DECL(7)
+MM_PASSK_DECL(8)
+#undef MM_PASSK_DECL
 
 namespace {
 
@@ -73,9 +78,6 @@ constexpr int kSeg = 0;                  // MODE value of the segment schedule
 #endif
 
 // input rows prefetched per wave: 8 KiB in flight for one attribute, ~8 KiB for more
-#ifndef MM_FMA_SHARE
-#define MM_FMA_SHARE 0  // interior cells: s = u*(r/8), u - out = fma(s, -8, u)
-#endif
 #ifndef MM_LEVEL_BARRIER
 #define MM_LEVEL_BARRIER 0  // scheduling barrier after every this many levels (0: none)
 #endif
@@ -111,8 +113,20 @@ __device__ __forceinline__ int span3k(long long n, long long i) {
     return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
 }
 
-__device__ __forceinline__ double share_k(double out, int cnt) {
-    return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
+// One emitter (oracle/mm_oracle.c emit): share s and kept value d = u - out; cnt == 8 as
+// s = u*(r/8), d = fma(s, -8, u) (equal to out/8 and u - out whenever out = r*u is normal).
+__device__ __forceinline__ void emit_k(double r, double u, int cnt, double& s, double& d) {
+    if (cnt == 8) {
+        s = u * (r * 0.125);
+        d = __builtin_fma(s, -8.0, u);
+    } else if (cnt > 0) {
+        const double out = r * u;
+        s = out / (double)cnt;
+        d = u - out;
+    } else {
+        s = 0.0;
+        d = u;
+    }
 }
 
 // Descriptor of `rows` consecutive rows starting at `first` (pointer already offset):
@@ -202,20 +216,12 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
             continue;
         }
         const double r = A.drate[a];
-        if (inner) {  // interior row, interior strip: cnt == 8
-#if MM_FMA_SHARE
+        if (inner) {  // interior row, interior strip: cnt == 8 (oracle/mm_oracle.c emit)
             const double r8 = r * 0.125;
             s0[a] = u0[a] * r8;
             s1[a] = u1[a] * r8;
             d0[a] = __builtin_fma(s0[a], -8.0, u0[a]);
             d1[a] = __builtin_fma(s1[a], -8.0, u1[a]);
-#else
-            const double o0 = r * u0[a], o1 = r * u1[a];
-            s0[a] = o0 * 0.125;
-            s1[a] = o1 * 0.125;
-            d0[a] = u0[a] - o0;
-            d1[a] = u1[a] - o1;
-#endif
         } else if (sx == 0) {  // row outside the grid
             s0[a] = s1[a] = 0.0;
             d0[a] = u0[a];
@@ -223,12 +229,8 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
         } else {
             const int k0 = c.sy0 ? sx * c.sy0 - 1 : 0;
             const int k1 = c.sy1 ? sx * c.sy1 - 1 : 0;
-            const double o0 = k0 > 0 ? r * u0[a] : 0.0;
-            const double o1 = k1 > 0 ? r * u1[a] : 0.0;
-            s0[a] = share_k(o0, k0);
-            s1[a] = share_k(o1, k1);
-            d0[a] = u0[a] - o0;
-            d1[a] = u1[a] - o1;
+            emit_k(r, u0[a], k0, s0[a], d0[a]);
+            emit_k(r, u1[a], k1, s1[a], d1[a]);
         }
     }
 }
@@ -618,6 +620,7 @@ hipError_t launch_k3(bool red, const PassArgs& a, hipStream_t s) {
     long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
     if (a.xcd_remap) blocks = (blocks + 7) / 8 * 8;
     const dim3 g((unsigned)blocks), b(kBlock);
+    (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
         hipLaunchKernelGGL((mm_passk_kernel<K, MODE, U, true, NT, NA, CHAIN>), g, b, 0, s, a);
     else
@@ -642,6 +645,7 @@ int seg_blocks_per_cu_v() {
     int n = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &n, mm_passk_kernel<K, kSeg, seg_prefetch<NA>(), RED, NT, NA, CHAIN>, kBlock, 0);
+    if (e != hipSuccess) (void)hipGetLastError();  // a failed query must not surface at the next launch
     return e == hipSuccess ? n : 0;
 }
 

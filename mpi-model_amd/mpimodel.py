@@ -32,8 +32,14 @@ EXPORTS = [
     "mm_point_apply", "mm_run", "mm_synchronize", "mm_sums", "mm_sums_history",
     "mm_clear_history", "mm_halo_export_rows", "mm_halo_import_rows", "mm_halo_export",
     "mm_halo_import", "mm_debug_read_rows",
-    "mm_set_timing", "mm_timing",
+    "mm_set_timing", "mm_timing", "mm_partition_rect_reference", "mm_owner_rect_reference",
+    "mm_wire_format_partition", "mm_wire_format_flow", "mm_wire_parse_partition",
+    "mm_wire_parse_flow", "mm_point_strict_applies", "mm_point_apply_strict",
 ]
+
+WIRE_LEN = 23
+TAG_PARTITION = 0
+TAG_FLOW = 999
 
 
 class MMError(RuntimeError):
@@ -104,6 +110,15 @@ def lib():
             "mm_halo_import": (I, [P, P, P]),
             "mm_debug_read_rows": (I, [P, I, LL, LL, P]),
             "mm_set_timing": (I, [P, I]),
+            "mm_partition_rect_reference": (I, [I, I, I, I, I, pI, pI, pI, pI]),
+            "mm_point_strict_applies": (I, [I, I, I, I, I]),
+            "mm_point_apply_strict": (I, [P, I, LL, LL, D, D, I, pI]),
+            "mm_owner_rect_reference": (I, [I, I, I]),
+            "mm_wire_format_partition": (I, [ctypes.c_char_p, I, I, I, I, I]),
+            "mm_wire_format_flow": (I, [ctypes.c_char_p, I, I, I, I, D]),
+            "mm_wire_parse_partition": (I, [ctypes.c_char_p, I, pI, pI, pI, pI]),
+            "mm_wire_parse_flow": (I, [ctypes.c_char_p, I, pI, pI, pI, pI,
+                                       ctypes.POINTER(D)]),
             "mm_timing": (I, [P, pLL, ctypes.POINTER(D), ctypes.POINTER(D)]),
         }
         for name, (res, args) in sig.items():
@@ -149,6 +164,45 @@ def partition_rows(H, G, g):
 
 def neighbor_count(H, W, x, y):
     return lib().mm_neighbor_count(H, W, x, y)
+
+
+def partition_rect_reference(H, W, lines, columns, k):
+    o = [ctypes.c_int() for _ in range(4)]
+    check(lib().mm_partition_rect_reference(H, W, lines, columns, k, *[ctypes.byref(x) for x in o]))
+    return tuple(x.value for x in o)  # x_init, y_init, height, width
+
+
+def point_strict_applies(H, W, P, x, y):
+    return lib().mm_point_strict_applies(H, W, P, x, y)
+
+
+def owner_rect_reference(space_height, x, y):
+    return lib().mm_owner_rect_reference(space_height, x, y)
+
+
+def wire_partition(x_init, y_init, height, width, length=WIRE_LEN):
+    buf = ctypes.create_string_buffer(length)
+    check(lib().mm_wire_format_partition(buf, length, x_init, y_init, height, width))
+    return buf.raw
+
+
+def wire_flow(owner, x, y, rate, length=WIRE_LEN):
+    buf = ctypes.create_string_buffer(length)
+    check(lib().mm_wire_format_flow(buf, length, owner, x, y, rate))
+    return buf.raw
+
+
+def parse_wire_partition(msg):
+    o = [ctypes.c_int() for _ in range(4)]
+    check(lib().mm_wire_parse_partition(msg, len(msg), *[ctypes.byref(x) for x in o]))
+    return tuple(x.value for x in o)
+
+
+def parse_wire_flow(msg):
+    o = [ctypes.c_int() for _ in range(4)]
+    r = ctypes.c_double()
+    check(lib().mm_wire_parse_flow(msg, len(msg), *[ctypes.byref(x) for x in o], ctypes.byref(r)))
+    return tuple(x.value for x in o) + (r.value,)  # owner, x, y, rate as atoi, rate
 
 
 def comm_id():
@@ -235,6 +289,14 @@ class Engine:
 
     def point_apply(self, sx, sy, captured, rate, attr=0):
         check(lib().mm_point_apply(self.ptr, attr, sx, sy, captured, rate))
+
+    def point_apply_strict(self, sx, sy, captured, rate, workers, attr=0):
+        """Strict-reference mode: applied only where the reference's run on `workers`
+        workers applies it (src/Model.hpp:189-216); returns whether it was applied."""
+        applied = ctypes.c_int()
+        check(lib().mm_point_apply_strict(self.ptr, attr, sx, sy, captured, rate, workers,
+                                          ctypes.byref(applied)))
+        return bool(applied.value)
 
     def run(self, nsteps, reduce_every=0):
         check(lib().mm_run(self.ptr, nsteps, reduce_every))

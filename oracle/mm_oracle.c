@@ -93,6 +93,25 @@ void or_point_apply(long long H, long long W, double* v, long long sx, long long
     v[sx * W + sy] = v[sx * W + sy] - out;          /* Model.hpp:211 */
 }
 
+/* One emitter of the whole-grid step: its share s and what it keeps, d = v - out.
+ * cnt == 8 (every interior cell): s = v * (rate/8) and d = fma(s, -8, v) -- with
+ * out = rate*v these are RN(out)/8 and RN(v - out) exactly (scaling by 2^-3 commutes with
+ * rounding and 8*s == RN(out)) whenever out is a normal number, and they save the device
+ * kernels one multiply per cell. Other counts: out = rate*v, s = out/cnt, d = v - out. */
+static inline void emit(double rate, double v, int cnt, double* s, double* d) {
+    if (cnt == 8) {
+        *s = v * (rate * 0.125);
+        *d = fma(*s, -8.0, v);
+    } else if (cnt > 0) {
+        double out = rate * v;
+        *s = out / (double)cnt;
+        *d = v - out;
+    } else {
+        *s = 0.0;
+        *d = v;
+    }
+}
+
 /* s row of global row gx (NULL vrow or outside grid -> +0.0) */
 static void s_row(long long H, long long W, long long gx, const double* vrow,
                   double rate, double* s) {
@@ -100,11 +119,8 @@ static void s_row(long long H, long long W, long long gx, const double* vrow,
         for (long long y = 0; y < W; ++y) s[y] = 0.0;
         return;
     }
-    for (long long y = 0; y < W; ++y) {
-        int cnt = or_neighbor_count(H, W, gx, y);
-        double out = cnt > 0 ? rate * vrow[y] : 0.0;
-        s[y] = share_of(out, cnt);
-    }
+    double d;
+    for (long long y = 0; y < W; ++y) emit(rate, vrow[y], or_neighbor_count(H, W, gx, y), &s[y], &d);
 }
 
 /* rows(gx) gives the v row for any global gx in [x_lo-1, x_hi]. */
@@ -133,10 +149,10 @@ static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
         if (v == NULL) {  /* output row outside the grid (or the slab): no cells, zeros */
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
         } else for (long long y = 0; y < W; ++y) {
-            int cnt = or_neighbor_count(H, W, x, y);
-            double out = cnt > 0 ? rate * v[y] : 0.0;
+            double sy, d;
+            emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
             double nb = (c3[y] + c3[y + 2]) + p[y];
-            o[y] = (v[y] - out) + nb;
+            o[y] = d + nb;
         }
         double* t = s_prev;
         s_prev = s_cur;

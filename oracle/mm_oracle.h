@@ -16,11 +16,14 @@
  *
  * Arithmetic contract (shared with the HIP kernels, compiled -ffp-contract=off):
  *   out(c) = r * v(c)                                   Exponencial.hpp:18-20
- *   s(c)   = out(c) / cnt(c)   (cnt==8: out*0.125, exact) Model.hpp:199
+ *   s(c)   = out(c) / cnt(c)                            Model.hpp:199
+ *   d(c)   = v(c) - out(c)                              Model.hpp:211
  *   p(c)   = s(x-1,y) + s(x+1,y)
  *   c3(c)  = p(c) + s(c)
  *   nb(c)  = (c3(x,y-1) + c3(x,y+1)) + p(c)
- *   v'(c)  = (v(c) - out(c)) + nb(c)                    Model.hpp:206-211,234
+ *   v'(c)  = d(c) + nb(c)                               Model.hpp:206-211,234
+ * computed for cnt == 8 as s = v*(r*0.125), d = fma(s, -8, v) -- the same two numbers
+ * whenever r*v is normal (2^-3 scaling is exact), one multiply fewer per cell.
  * s is +0.0 outside the global grid; cnt is the number of in-grid Moore
  * neighbours (Cell.hpp:71-157 gives 3/5/8 for grids of at least 2x2).
  */

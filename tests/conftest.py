@@ -57,3 +57,9 @@ def golden(name):
 def golden_points():
     import glob
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "point_*.json")))
+
+
+def golden_strict():
+    """Sources off the reference's valid domain that it still completes (no cell changed)."""
+    import glob
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "strict_*.json")))

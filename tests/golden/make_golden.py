@@ -10,13 +10,18 @@ differs from the reference's init value 1.0 (Model.hpp:155), as exact hex floats
 Cases stay inside the reference's valid oracle domain:
 source row == PROC_DIMX-1 (last row of worker 1's slab), interior column.
 
-Two fixture kinds:
+Three fixture kinds:
   point_<geom>_<n>.json  exact grids from oracle/_ref/ref_<geom> (our driver over
                          the unmodified reference headers, hex-float dump)
   c1_default_text.json   the reference's own Main.cpp build: sha256 + the
                          non-trivial lines of every comm_rank%d.txt it writes at
                          default ostream precision (Model.hpp:246-257) -- the
                          byte-level format the drop-in writer must reproduce.
+  wire_<model>_<geom>_<n>.json  every MPI_Send the reference makes (oracle/_ref/wire_*:
+                         oracle/ref_wire_harness.cpp interposes MPI_Send over the unmodified
+                         reference headers): the 23-char partition / flow descriptors of
+                         Model (src/Model.hpp:70-86) and ModelRectangular's 2-D blocks
+                         (src/ModelRectangular.hpp:69-92), halo scalars, sums, file names.
 """
 import hashlib
 import json
@@ -92,6 +97,65 @@ def point_case(geom, sx, sy, value, rate):
     }
 
 
+# Sources OUTSIDE the valid domain that the reference still completes (SURVEY.md section
+# 0: other sources crash or hang): with one worker, or in the last of two workers' slabs,
+# it changes no cell (src/Model.hpp:189-216). Pins the strict-reference point mode.
+STRICT_CASES = [
+    ("24_16_1", 11, 7, "2.0", "0.5"),    # interior, not the slab's last row
+    ("24_16_1", 23, 7, "2.0", "0.5"),    # the slab's last row = the grid's: 5 neighbours
+    ("24_16_1", 0, 5, "2.0", "0.5"),     # top edge
+    ("24_16_1", 23, 15, "2.0", "0.5"),   # corner: 3 neighbours
+    ("30_20_1", 14, 9, "1.5", "0.25"),
+    ("30_20_1", 29, 10, "1.5", "0.25"),
+    ("24_16_2", 15, 7, "2.0", "0.5"),    # last worker, interior, not its last row
+    ("24_16_2", 20, 8, "3.0", "0.1"),
+    ("24_16_2", 23, 0, "2.0", "0.5"),
+]
+
+# (model, geometry, np, src_x, src_y, value, rate, space h/w or None)
+WIRE_CASES = [
+    ("row", "100_100_5", 6, 19, 3, "2.2", "0.1", None),       # Main.cpp:33 default
+    ("row", "40_64_4", 5, 9, 17, "3.5", "0.25", None),
+    ("rect", "20_60_2_3", 7, 18, 19, "2.2", "0.1", None),     # Main.cpp:37-47 (commented)
+    ("rect", "24_60_3_2", 7, 5, 7, "1.5", "0.3", None),
+    ("rect", "20_61_2_3", 7, 3, 4, "1.0", "0.5", None),       # DIMY_REC % COLUMNS_REC != 0
+    ("rect", "30_40_3_4", 13, 7, 11, "2.0", "0.2", (12, 9)),
+]
+
+
+def wire_case(model, geom, np_, sx, sy, value, rate, space):
+    binary = os.path.join(REF_DIR, f"wire_{model}_{geom}")
+    args = [model, str(sx), str(sy), value, rate] + ([str(space[0]), str(space[1])] if space else [])
+    work = tempfile.mkdtemp(prefix="mmwire_")
+    os.makedirs(os.path.join(work, "run"))
+    os.makedirs(os.path.join(work, "output"))
+    proc = subprocess.run([MPIRUN, "-np", str(np_), binary] + args, cwd=os.path.join(work, "run"),
+                          capture_output=True, text=True, timeout=60)
+    shutil.rmtree(work)
+    if proc.returncode != 0:
+        raise RuntimeError(f"{binary} failed: {proc.stderr[-2000:]}")
+    sends = {}
+    for ln in proc.stderr.splitlines():
+        if not ln.startswith("MPISEND "):
+            continue
+        f = dict(kv.split("=", 1) for kv in ln[8:].split(" ", 5))
+        sends.setdefault(int(f["src"]), []).append(
+            [int(f["dest"]), int(f["tag"]), f["type"], int(f["count"]), f["data"]])
+    dims = [int(t) for t in geom.split("_")]
+    fx = {"kind": "wire", "model": model, "np": np_, "src_x": sx, "src_y": sy,
+          "value": value, "rate": rate,
+          "sends_by_rank": {str(k): v for k, v in sorted(sends.items())},
+          "reference_stdout_lines": sorted(proc.stdout.splitlines()),
+          "generator": f"oracle/_ref/wire_{model}_{geom} (oracle/ref_wire_harness.cpp over "
+                       f"/root/reference/src)"}
+    if model == "row":
+        fx.update(dimx=dims[0], dimy=dims[1], nworkers=dims[2])
+    else:
+        fx.update(dimx_rec=dims[0], dimy_rec=dims[1], lines_rec=dims[2], columns_rec=dims[3],
+                  space=list(space) if space else [dims[0] // dims[2], dims[1] // dims[3]])
+    return fx
+
+
 def c1_text_case():
     stdout, files = run_ref(os.path.join(REF_DIR, "ref_main_default"), 6, [])
     ranks = {}
@@ -133,6 +197,21 @@ def main():
             json.dump(fx, f, indent=1)
         index.append(name)
         print(name, len(fx["changed"]), "cells changed")
+    for i, (geom, sx, sy, value, rate) in enumerate(STRICT_CASES):
+        fx = point_case(geom, sx, sy, value, rate)
+        fx["kind"] = "strict"
+        name = f"strict_{geom}_{i}.json"
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump(fx, f, indent=1)
+        index.append(name)
+        print(name, len(fx["changed"]), "cells changed")
+    for i, case in enumerate(WIRE_CASES):
+        fx = wire_case(*case)
+        name = f"wire_{case[0]}_{case[1]}_{i}.json"
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump(fx, f, indent=1)
+        index.append(name)
+        print(name, sum(len(v) for v in fx["sends_by_rank"].values()), "messages")
     fx = c1_text_case()
     with open(os.path.join(HERE, "c1_default_text.json"), "w") as f:
         json.dump(fx, f, indent=1)

@@ -84,3 +84,86 @@ def test_bad_arguments_are_errors(mm):
 def test_engine_refuses_to_start_without_gpu(mm):
     with pytest.raises(mm.MMError):
         mm.Engine(16, 16)
+
+
+# ---- the reference's control plane, pinned by its own MPI traffic -------------------
+# tests/golden/wire_*.json: every MPI_Send of the reference, recorded by
+# oracle/ref_wire_harness.cpp (MPI_Send interposed over the unmodified reference headers).
+
+def wire_fixtures():
+    import glob
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(REPO, "tests", "golden", "wire_*.json")))
+
+
+def master_messages(g, tag):
+    return [(d, data) for d, t, typ, n, data in g["sends_by_rank"]["0"] if t == tag and typ == "char"]
+
+
+@pytest.mark.parametrize("name", wire_fixtures())
+def test_wire_partition_descriptors_match_reference(mm, name):
+    from conftest import golden
+    g = golden(name)
+    msgs = master_messages(g, mm.TAG_PARTITION)
+    P = g["np"] - 1
+    assert [d for d, _ in msgs] == list(range(1, P + 1))
+    for k, data in msgs:
+        if g["model"] == "row":
+            desc = mm.partition_reference(g["dimx"], g["dimy"], P, k)
+        else:
+            desc = mm.partition_rect_reference(g["dimx_rec"], g["dimy_rec"], g["lines_rec"],
+                                               g["columns_rec"], k)
+        raw = mm.wire_partition(*desc)
+        assert len(raw) == mm.WIRE_LEN and raw.rstrip(b"\0").decode() == data, (k, desc, data)
+        assert mm.parse_wire_partition(data.encode()) == desc  # src/Model.hpp:139-146
+
+
+@pytest.mark.parametrize("name", wire_fixtures())
+def test_wire_flow_descriptors_match_reference(mm, name):
+    from conftest import golden
+    g = golden(name)
+    msgs = master_messages(g, mm.TAG_FLOW)
+    P = g["np"] - 1
+    sx, sy, rate = g["src_x"], g["src_y"], float(g["rate"])
+    if g["model"] == "row":
+        owner = mm.owner_reference(g["dimx"], P, sx)  # src/Model.hpp:80
+    else:
+        owner = mm.owner_rect_reference(g["space"][0], sx, sy)  # src/ModelRectangular.hpp:85
+    want = mm.wire_flow(owner, sx, sy, rate).rstrip(b"\0").decode()
+    assert [d for d, _ in msgs] == list(range(1, P + 1))
+    assert all(data == want for _, data in msgs)
+    # the worker's parse: owner, x, y by atoi, and the rate read back as an int (atoi)
+    assert mm.parse_wire_flow(want.encode())[:4] == (owner, sx, sy, int(rate) if rate >= 1 else 0)
+    assert mm.parse_wire_flow(want.encode())[4] == float(f"{rate:f}")
+    # the master prints the descriptor (src/Model.hpp:82; ModelRectangular adds the owner)
+    line = want if g["model"] == "row" else f"{want} {owner}"
+    assert line in g["reference_stdout_lines"]
+
+
+def test_wire_format_refuses_overflow(mm):
+    with pytest.raises(mm.MMError):  # the reference's sprintf would overrun its 23 chars
+        mm.wire_partition(2 ** 30, 2 ** 30, 2 ** 30, 2 ** 30)
+    with pytest.raises(mm.MMError):
+        mm.parse_wire_flow(b"12")
+
+
+def test_rect_partition_without_wrap(mm):
+    # DIMY_REC % COLUMNS_REC != 0: the column offset never lands on DIMY_REC, so the
+    # reference never moves to the second band of rows (src/ModelRectangular.hpp:76-79)
+    assert [mm.partition_rect_reference(20, 61, 2, 3, k)[:2] for k in range(1, 7)] == \
+        [(0, 0), (0, 20), (0, 40), (0, 60), (0, 80), (0, 100)]
+
+
+def point_fixtures(prefix):
+    import glob
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(REPO, "tests", "golden", prefix + "_*.json")))
+
+
+@pytest.mark.parametrize("name", point_fixtures("point") + point_fixtures("strict"))
+def test_strict_point_decision_matches_reference(mm, name):
+    # src/Model.hpp:176-235: the reference changes cells only for an interior source on
+    # its owner's last row; off that domain (strict_*: sources the reference still
+    # completes) it changes nothing
+    from conftest import golden
+    g = golden(name)
+    applies = mm.point_strict_applies(g["dimx"], g["dimy"], g["nworkers"], g["src_x"], g["src_y"])
+    assert applies == (1 if g["changed"] else 0)

@@ -60,15 +60,101 @@ def test_default_run_matches_reference_output_files(tmp_path, binary):
         assert line in stdout.splitlines()
 
 
-@pytest.mark.parametrize("np_", [1, 3])
+@pytest.mark.parametrize("np_", [1, 2, 3])
 def test_default_run_other_layouts(tmp_path, np_):
-    # one process (master = only worker) and 2 workers: same cells, same bytes in order
+    # one process (master = only worker), 1 and 2 workers: same cells, same bytes in order.
+    # np 2 is BASELINE.json configs[0] ("mpirun -np 2"), where the reference itself
+    # overflows its static cell array
     g = golden("c1_default_text.json")
     _, files = run_mpi(tmp_path, os.path.join(REPO, "examples", "drop_in_main"), np_)
     ranks = sorted(k for k in files if k.startswith("comm_rank"))
     assert len(ranks) == max(np_ - 1, 1)
     cat = b"".join(files[k] for k in sorted(ranks, key=lambda s: int(s[9:-4])))
     assert hashlib.sha256(cat).hexdigest() == g["concat_sha256"]
+
+
+def test_reference_main_at_np2(tmp_path):
+    # the reference's own src/Main.cpp, unchanged, over our headers at BASELINE.json
+    # configs[0]'s layout: one worker owns the whole grid
+    ref = os.path.join(REPO, "oracle", "_ref", "dropin_ref_main")
+    if not os.path.exists(ref):
+        pytest.skip("dropin_ref_main is built only where /root/reference exists")
+    g = golden("c1_default_text.json")
+    stdout, files = run_mpi(tmp_path, ref, 2)
+    assert sorted(k for k in files if k.startswith("comm_rank")) == ["comm_rank1.txt"]
+    assert hashlib.sha256(files["comm_rank1.txt"]).hexdigest() == g["concat_sha256"]
+    assert "1|19:3|0.100000" in stdout.splitlines()
+
+
+def mpi_sends(stderr):
+    out = {}
+    for ln in stderr.splitlines():
+        if ln.startswith("MPISEND "):
+            f = dict(kv.split("=", 1) for kv in ln[8:].split(" ", 5))
+            out.setdefault(int(f["src"]), []).append(
+                [int(f["dest"]), int(f["tag"]), f["type"], int(f["count"]), f["data"]])
+    return out
+
+
+def run_logged(tmp_path, binary, np_, args=()):
+    run = tmp_path / "run"
+    out = tmp_path / "output"
+    run.mkdir()
+    out.mkdir()
+    p = subprocess.run([MPIRUN, "-np", str(np_), binary] + [str(a) for a in args], cwd=run,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    files = {os.path.basename(f): open(f, "rb").read() for f in glob.glob(str(out / "*"))}
+    return p.stdout, mpi_sends(p.stderr), files
+
+
+def test_dropin_control_messages_match_reference(tmp_path):
+    # the drop-in driver speaks the reference's wire protocol: the master's 23-char
+    # partition / flow descriptors (src/Model.hpp:70-86) and the workers' sums and file
+    # names (src/Model.hpp:243,260), against the reference's own traffic
+    # (tests/golden/wire_row_100_100_5_0.json, recorded from the reference binary)
+    g = golden("wire_row_100_100_5_0.json")
+    binary = os.path.join(REPO, "oracle", "_build", "dropin_wire_main")
+    stdout, sends, _ = run_logged(tmp_path, binary, g["np"])
+    ref = g["sends_by_rank"]
+    want = [m for m in ref["0"] if m[2] == "char"]
+    got = [m for m in sends[0] if m[2] == "char" and m[1] in (0, 999)]
+    assert got == want
+    for k in range(1, g["np"]):
+        rs = [m for m in ref[str(k)] if m[0] == 0]  # worker -> master: sum, file name
+        gs = [m for m in sends[k] if m[0] == 0 and m[1] == k]
+        assert [m[:4] for m in gs] == [m[:4] for m in rs], k
+        a, b = float.fromhex(gs[0][4]), float.fromhex(rs[0][4])
+        assert abs(a - b) <= 1e-12 * b  # slab sums: device reduction vs serial loop
+        assert gs[1][4] == rs[1][4]  # "../output/comm_rank<k>.txt"
+    for line in g["reference_stdout_lines"]:
+        assert line in stdout.splitlines()
+
+
+def test_rect_model_matches_reference(tmp_path):
+    # ModelRectangular (src/ModelRectangular.hpp:52-272) on the reference's defaults
+    # (20 x 60 cells, 2 x 3 blocks, -np 7, source (18,19)): the same block descriptors and
+    # flow descriptor on the wire, the same printed lines, no result files (as the
+    # reference); MPI_Report carries the descriptors and the owner
+    import json
+    g = golden("wire_rect_20_60_2_3_2.json")
+    binary = os.path.join(REPO, "oracle", "_build", "rect_wire_main")
+    stdout, sends, files = run_logged(tmp_path, binary, g["np"])
+    want = [m for m in g["sends_by_rank"]["0"] if m[2] == "char"]
+    got = [m for m in sends[0] if m[2] == "char" and m[1] in (0, 999)]
+    assert got == want
+    lines = stdout.splitlines()
+    owner = int(want[-1][4].split("|")[0])
+    assert lines.count(f"{want[-1][4]} {owner}") == 1          # master, :88
+    assert lines.count(want[-1][4]) == g["np"] - 1             # every worker, :158
+    assert f"{owner}: 0.22" in lines                           # the owner, :180
+    assert not files
+    rep = json.loads([ln for ln in lines if ln.startswith("{")][-1])
+    assert rep["owner"] == owner
+    descs = [[int(t) for t in m[4].replace(":", "|").split("|")] for m in want if m[1] == 0]
+    assert rep["blocks"] == descs
+    # the point flow itself changes no total
+    assert float.fromhex(rep["final_sum"]) == 20 * 60
 
 
 @pytest.mark.parametrize("np_", [1, 3, 4])

@@ -46,7 +46,7 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
         s0 = e.sums()[0]
         e.add_diffuse(0, RATE)
         info = e.info()
-        assert info["steps_per_launch"] == 4 and info["kernel"] == 2
+        assert info["steps_per_launch"] >= 4 and info["kernel"] == 2
         e.run(STEPS)
         e.synchronize()
         s1 = e.sums()[0]

@@ -14,6 +14,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                            \
@@ -35,6 +36,7 @@ struct Args {
     int R;          // rows per wave (layout 0) / row groups G (layout 1)
     long long nstrips, waves;
     int layout, mode;
+    long long pitch;  // row stride in doubles (>= W)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* p, long long bytes) {
@@ -59,13 +61,13 @@ __global__ __launch_bounds__(256) void walk(Args a) {
         rstep = a.R;
         n = (int)((a.H - q + a.R - 1) / a.R);
     }
-    const long long rowb = a.W * 8;
+    const long long rowb = a.pitch * 8;
     const unsigned voff = (unsigned)((strip * 128 + 2 * lane) * 8);
     const unsigned step = (unsigned)(rstep * rowb);
     // descriptors rebuilt every U rows at the current row: offsets stay below 2^31
     auto desc = [&](const double* base, int r) {
         const long long rem = (long long)(n - r) * rstep * rowb;
-        return rsrc(base + (long long)r * rstep * a.W + r0 * a.W, rem < 0x7fffffffLL ? rem : 0x7fffffffLL);
+        return rsrc(base + (long long)r * rstep * a.pitch + r0 * a.pitch, rem < 0x7fffffffLL ? rem : 0x7fffffffLL);
     };
     __amdgpu_buffer_rsrc_t ri = desc(a.in, 0), ro = desc(a.out, 0);
     dv2 buf[U];
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void walk(Args a) {
     }
     if (a.mode == 1)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc),
-                                               rsrc(a.out + r0 * a.W, rowb), voff, 0, 2);
+                                               rsrc(a.out + r0 * a.pitch, rowb), voff, 0, 2);
     if (lane == 64) lds_pad[0] = acc.x;  // keep the LDS allocation (never executed)
 }
 
@@ -237,10 +239,34 @@ float run_split(const Args& a0, int reps) {
 int main(int argc, char** argv) {
     const long long H = argc > 1 ? atoll(argv[1]) : 32768, W = argc > 2 ? atoll(argv[2]) : 32768;
     double *a, *b;
-    CK(hipMalloc(&a, H * W * 8));
-    CK(hipMalloc(&b, H * W * 8));
-    CK(hipMemset(a, 0, H * W * 8));
-    CK(hipMemset(b, 0, H * W * 8));
+    const long long maxpitch = W + (argc > 4 ? 32768 : 4096);
+    CK(hipMalloc(&a, H * maxpitch * 8));
+    CK(hipMalloc(&b, H * maxpitch * 8));
+    CK(hipMemset(a, 0, H * maxpitch * 8));
+    CK(hipMemset(b, 0, H * maxpitch * 8));
+    if (argc > 3 && std::string(argv[3]) == "pitch") {
+        std::vector<int> pads;
+        for (int i = 4; i < argc; ++i) pads.push_back(atoi(argv[i]));
+        if (pads.empty()) pads = {0, 64, 128, 256, 1024, 4096};
+        for (int pad : pads)
+            for (int mode : {0, 2})
+                for (int R : {8, 2048}) {
+                    Args a0{a, b, H, W, R, W / 128, (W / 128) * ((H + R - 1) / R), 0, mode, W + pad};
+                    const float t = run<8>(a0, 0, 6);
+                    const double bytes = (mode == 0 ? 16.0 : 8.0) * H * W;
+                    std::printf("pitch W+%d R=%d mode=%s : %.1f us %.0f GB/s\n", pad, R,
+                                mode == 0 ? "copy" : "store", t * 1e3, bytes / t / 1e6);
+                }
+        if (argc > 4) return 0;
+        for (int pad : {0, 128, 1024})
+            for (int R : {512, 2048}) {
+                Args a0{a, b, H, W, R, W / 128, (W / 128) * ((H + R - 1) / R), 0, 0, W + pad};
+                const float t = run<32>(a0, 160, 6);
+                std::printf("pitch W+%d R=%d U=32 lds_kb=160 copy : %.1f us %.0f GB/s\n", pad, R,
+                            t * 1e3, 16.0 * H * W / t / 1e6);
+            }
+        return 0;
+    }
     const long long ns = W / 128;
     const char* mname[] = {"copy", "load", "store"};
     std::printf("grid %lldx%lld, GB/s counted as 16 B per cell (copy), 8 B (load/store only)\n", H, W);
@@ -253,7 +279,7 @@ int main(int argc, char** argv) {
     for (int G : {8, 16, 64})
         for (int lds : {0, 80}) cfgs.push_back({1, G, lds >= 80 ? 16 : 8, lds, 0});
     for (const Cfg& c : cfgs) {
-        Args a0{a, b, H, W, c.R, ns, 0, c.layout, c.mode};
+        Args a0{a, b, H, W, c.R, ns, 0, c.layout, c.mode, W};
         a0.waves = c.layout == 0 ? ns * ((H + c.R - 1) / c.R) : ns * c.R;
         float t = c.U == 8 ? run<8>(a0, c.lds_kb, 6) : (c.U == 16 ? run<16>(a0, c.lds_kb, 6) : run<32>(a0, c.lds_kb, 6));
         const double bytes = (c.mode == 0 ? 16.0 : 8.0) * H * W;
@@ -263,7 +289,7 @@ int main(int argc, char** argv) {
     }
     // decoupled stores (producer / consumer waves through LDS)
     auto split = [&](const char* name, float (*f)(const Args&, int), int R) {
-        Args a0{a, b, H, W, R, ns, 0, 0, 0};
+        Args a0{a, b, H, W, R, ns, 0, 0, 0, W};
         const float t = f(a0, 6);
         std::printf("split %s R=%d : %.1f us %.0f GB/s\n", name, R, t * 1e3, 16.0 * H * W / t / 1e6);
     };
@@ -278,7 +304,7 @@ int main(int argc, char** argv) {
     // cache policy of the loads / stores (aux bits: 1 sc0, 2 nt, 16 sc1) on long copies
     std::printf("policy sweep: layout 0, R=2048, copy\n");
     auto pol = [&](const char* name, float (*f)(const Args&, int, int), int U, int lds) {
-        Args a0{a, b, H, W, 2048, ns, ns * ((H + 2047) / 2048), 0, 0};
+        Args a0{a, b, H, W, 2048, ns, ns * ((H + 2047) / 2048), 0, 0, W};
         const float t = f(a0, lds, 6);
         std::printf("policy %s U=%d lds_kb=%d : %.1f us %.0f GB/s\n", name, U, lds, t * 1e3,
                     16.0 * H * W / t / 1e6);
