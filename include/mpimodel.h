@@ -96,6 +96,7 @@ typedef struct mm_info {
     long long graph_launches;  /* hipGraphLaunch calls so far */
     long long hist_entries;    /* step-sum history entries enqueued (MPI_Report) */
     char graph_note[160];      /* why capture was refused ("" otherwise) */
+    int seg_waves_per_cu;      /* resident waves per CU the K-step segment plan assumes */
 } mm_info;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */

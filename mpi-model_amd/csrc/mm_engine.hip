@@ -100,7 +100,7 @@ struct mm_engine {
 
     int th = 8;              // rows per wave, one-step kernel
     bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
-    int kpass = 7;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps)
+    int kpass = 0;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps; 0: auto)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
     double seg_waves = 2.0;  // segment waves per resident wave slot (MM_SEG_WAVES)
     double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
@@ -478,7 +478,11 @@ bool passk_ok(const mm_engine* e) {
 // Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
 // past the thinnest slab of the chain (every rank sends K owned rows each way).
 int passk_steps(const mm_engine* e) {
-    int k = e->na == 1 ? e->kpass : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
+    // one attribute, auto: K = 8 on slabs of >= 2^28 cells, else 7 -- the fastest K of
+    // the round-2 sweeps (profiles/r02/sweep_k_*.log: 32768^2 and 16384^2 favour 8, 4096^2
+    // with its short segments 7; K <= 4 leaves the VALU idle behind the HBM stream)
+    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->d.h * (double)e->d.W >= 268435456.0 ? 8 : 7);
+    int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
     if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
     return std::max(1, k);
 }
@@ -852,6 +856,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         info->rows_per_wave = A.th;
         info->waves_per_pass = A.waves_total;
         info->kernel = 2;
+        info->seg_waves_per_cu = e->wpc[0][e->variant & 1][e->na][spl];
     } else {
         info->kernel = 0;
         info->rows_per_wave = e->th;

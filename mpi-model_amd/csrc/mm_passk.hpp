@@ -45,6 +45,8 @@
 // translation unit per K so the builds run in parallel) and mm_kernels_k.hip dispatches.
 #pragma once
 
+#include <algorithm>
+
 #include "mm_internal.hpp"
 
 namespace mm {
@@ -84,9 +86,12 @@ constexpr int kSeg = 0;                  // MODE value of the segment schedule
 #ifndef MM_SEG_U1
 #define MM_SEG_U1 8  // rows prefetched per wave, one attribute
 #endif
+#ifndef MM_SEG_UN
+#define MM_SEG_UN 2  // rows prefetched per wave, three or four attributes
+#endif
 template <int NA>
 constexpr int seg_prefetch() {
-    return NA == 1 ? MM_SEG_U1 : (NA == 2 ? 4 : 2);
+    return NA == 1 ? MM_SEG_U1 : (NA == 2 ? 4 : MM_SEG_UN);
 }
 
 // mov_dpp has no tied "old" operand, so the result can land in a fresh register without
@@ -640,13 +645,23 @@ hipError_t launch_k2(bool red, const PassArgs& a, hipStream_t s, int v) {
                    : launch_k3<K, kSeg, U, 0, NA, CHAIN>(red, a, s);
 }
 
+// Resident blocks per CU of the segment kernel, from its register count: gfx950 gives each
+// SIMD lane 512 registers (VGPRs and AGPRs together, allocated in granules of 8), at most
+// 8 waves per SIMD, 4 SIMDs per CU (MI355X_MICROARCH.md). The runtime's occupancy query is
+// not used: after `import torch` it answers for this kernel with half the true occupancy
+// (profiles/r02/occupancy_probe.log), which would halve the waves of every plan.
 template <int K, int NA, bool CHAIN, bool RED, int NT>
 int seg_blocks_per_cu_v() {
-    int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mm_passk_kernel<K, kSeg, seg_prefetch<NA>(), RED, NT, NA, CHAIN>, kBlock, 0);
-    if (e != hipSuccess) (void)hipGetLastError();  // a failed query must not surface at the next launch
-    return e == hipSuccess ? n : 0;
+    hipFuncAttributes fa;
+    const hipError_t e = hipFuncGetAttributes(
+        &fa, reinterpret_cast<const void*>(mm_passk_kernel<K, kSeg, seg_prefetch<NA>(), RED, NT, NA, CHAIN>));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // a failed query must not surface at the next launch
+        return 0;
+    }
+    const int regs = (fa.numRegs + 7) / 8 * 8;
+    const int waves_per_simd = regs > 0 ? std::min(8, 512 / regs) : 8;
+    return waves_per_simd * 4 / kWavesPerBlock;
 }
 
 template <int K, int NA, bool CHAIN>

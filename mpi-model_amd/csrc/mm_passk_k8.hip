@@ -1,12 +1,12 @@
 // mm_passk_k8.hip -- instances of the K-step kernel (mm_passk.hpp) for K = 8 (one attribute).
-// Tuning (tools/libsweep.py, profiles/r02): two waves per SIMD (<= 256 VGPRs) and 6 rows
-// prefetched per wave; with the register file's other half a second wave hides the
-// K-level VALU chains.
+// Tuning (tools/libsweep.py, profiles/r02): two waves per SIMD (<= 256 VGPRs) and 4 rows
+// prefetched per wave (6 spill at K = 8); with the register file's other half a second
+// wave hides the K-level VALU chains.
 #ifndef MM_PASSK_MIN_WAVES
 #define MM_PASSK_MIN_WAVES 2
 #endif
 #ifndef MM_SEG_U1
-#define MM_SEG_U1 6
+#define MM_SEG_U1 4
 #endif
 #include "mm_passk.hpp"
 

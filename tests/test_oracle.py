@@ -161,3 +161,14 @@ def test_program_step_conserves_total(O):
     t0 = math.fsum(np.concatenate([f.ravel() for f in fields]))
     t1 = math.fsum(np.concatenate([f.ravel() for f in out]))
     assert abs(t1 - t0) <= 1e-12 * t0
+
+
+def test_oracle_under_address_and_ub_sanitizers(O):
+    """the restatement under ASan + UBSan (oracle/oracle_selftest.c:
+    every function on degenerate and ragged grids, slab = whole-grid step, conservation)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", O.HERE, "asan"], check=True)
+    r = subprocess.run([os.path.join(O.HERE, "_build", "oracle_selftest_asan")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "oracle selftest ok" in r.stdout

@@ -38,6 +38,35 @@ def child(a):
         ok = np.array_equal(e.download(), O.field_step(O.fill_random(H, W), 0.3, steps=9))
     out["bit_exact"] = bool(ok)
     H = W = a.size
+    if a.program == "c5":  # config C5: 4 attributes, chained transfers + 4 diffusions, sums
+        flows = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
+                 (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+        h, w = 67, 300
+        fields = [O.fill_random(h, w, seed=O.SEED + k) for k in range(4)]
+        want = O.program_step(fields, flows, steps=5)
+        with mm.Engine(h, w, n_attr=4) as e:
+            for k in range(4):
+                e.fill_random(k, seed=O.SEED + k)
+            for kind, x, y, r in flows:
+                (e.add_diffuse(x, r) if kind == 1 else e.add_transfer(x, y, r))
+            e.run(5, 1)
+            out["bit_exact"] = out["bit_exact"] and all(
+                np.array_equal(e.download(k), want[k]) for k in range(4))
+        with mm.Engine(H, W, n_attr=4) as e:
+            for k in range(4):
+                e.fill_random(k, seed=O.SEED + k)
+            for kind, x, y, r in flows:
+                (e.add_diffuse(x, r) if kind == 1 else e.add_transfer(x, y, r))
+            e.run(8, 1)
+            e.set_timing(True)
+            e.run(a.steps, 1)
+            n, ms, b = e.timing()
+            e.set_timing(False)
+            info = e.info()
+        out.update(kernel_ms=ms / n, bytes=b, spl=info["steps_per_launch"],
+                   rows=info["rows_per_wave"], waves=info["waves_per_pass"])
+        print("RESULT " + json.dumps(out), flush=True)
+        return
     with mm.Engine(H, W) as e:
         e.fill_random(0)
         e.add_diffuse(0, 0.1)
@@ -59,6 +88,7 @@ def main():
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--env", default="{}")
+    ap.add_argument("--program", default="", help="c5: the 4-attribute flow program")
     ap.add_argument("--lib", default="")
     ap.add_argument("--timeout", type=int, default=120)
     a = ap.parse_args()
@@ -68,7 +98,7 @@ def main():
     for rnd in range(a.rounds):
         for lib in a.libs:
             cmd = [sys.executable, "-u", __file__, "--lib", lib, "--size", str(a.size),
-                   "--steps", str(a.steps), "--env", a.env]
+                   "--steps", str(a.steps), "--env", a.env, "--program", a.program]
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
             if p.returncode != 0 or not line:
