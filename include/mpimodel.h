@@ -212,6 +212,10 @@ int mm_point_apply_strict(mm_engine* eng, int attr, long long sx, long long sy,
  * the caller exchanges halo_depth rows (mm_halo_export_rows / mm_halo_import_rows)
  * between calls, and the engine runs the same interior / border split as with RCCL. */
 int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
+/* Do the one-time work of a following mm_run(eng, nsteps, reduce_every) now -- capture and
+ * instantiate its hipGraph, plan its eager tail passes (loading their kernels) -- without
+ * running any step. Optional: mm_run does the same work on first use. */
+int mm_prepare(mm_engine* eng, long long nsteps, long long reduce_every);
 int mm_synchronize(mm_engine* eng);
 
 /* Sums of the owned cells. mm_sums reduces the CURRENT state now (synchronous).

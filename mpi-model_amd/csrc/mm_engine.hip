@@ -963,17 +963,78 @@ int mm_point_apply_strict(mm_engine* e, int attr, long long sx, long long sy, do
     return mm_point_apply(e, attr, sx, sy, captured, rate);
 }
 
-int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
-    if (!e || nsteps < 0 || reduce_every < 0) return fail(MM_ERR_INVALID, "mm_run: bad arguments");
+}  // extern "C"
+
+namespace {
+
+// Graph plan of a run of nsteps steps: `per` steps per replayed graph (0: run eagerly).
+// A graph holds a whole number of K-step passes, an even number of buffer flips (so the
+// captured pointers are valid again) and of reduction periods (so the phase is the same at
+// every replay).
+long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every) {
+    const long long unit = steps_per_launch(e);
+    const long long flips = passk_ok(e) ? 1 : (long long)e->passes.size();
+    long long len = unit * ((flips % 2) ? 2 : 1);
+    if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
+    if (len > 256 || nsteps < len || !e->graphs_ok) return 0;
+    long long per = len;
+    while (per < 16 && per * 2 <= nsteps) per *= 2;
+    return per;
+}
+
+int check_run(mm_engine* e, long long nsteps, long long reduce_every, const char* who) {
+    if (!e || nsteps < 0 || reduce_every < 0) return fail(MM_ERR_INVALID, std::string(who) + ": bad arguments");
     if (nsteps == 0) return MM_OK;
-    if (e->passes.empty()) return fail(MM_ERR_STATE, "mm_run: no flow added (mm_add_flow)");
+    if (e->passes.empty()) return fail(MM_ERR_STATE, std::string(who) + ": no flow added (mm_add_flow)");
     if (e->d.halo_mode == MM_HALO_HOST && e->d.nranks > 1) {
         if (e->passes.size() != 1)
-            return fail(MM_ERR_STATE, "mm_run: the host halo transport runs one-pass flow programs only");
+            return fail(MM_ERR_STATE, std::string(who) + ": the host halo transport runs one-pass flow programs only");
         if (nsteps > halo_depth(e))
-            return fail(MM_ERR_STATE, "mm_run: host halo transport: at most halo_depth steps per "
+            return fail(MM_ERR_STATE, std::string(who) + ": host halo transport: at most halo_depth steps per "
                                       "call (exchange halo_depth rows between calls)");
     }
+    return MM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
+    MM_TRY(check_run(e, nsteps, reduce_every, "mm_prepare"));
+    if (nsteps == 0) return MM_OK;
+    MM_TRY(set_device(e));
+    const long long phase = reduce_every > 0 ? e->steps_done % reduce_every : 0;
+    const long long per = e->timing ? 0 : graph_per(e, nsteps, reduce_every);
+    long long tail = nsteps;
+    if (per > 0) {
+        hipGraphExec_t g = nullptr;
+        if (get_graph(e, per, reduce_every, phase, &g) != MM_OK) {
+            e->graph_note = g_last_error;
+            (void)hipGetLastError();
+            e->graphs_ok = false;
+            e->graph_state = -1;
+        } else {
+            tail = nsteps % per;
+        }
+    }
+    // the eagerly launched passes: plan them now, which loads their kernels' code objects
+    if (passk_ok(e) && tail > 0) {
+        const int kp = passk_steps(e);
+        for (long long s = 0; s < tail; s += kp) {
+            const int k = (int)std::min<long long>(kp, tail - s);
+            mm::PassArgs A;
+            std::memset(&A, 0, sizeof A);
+            A.nstrips = (int)nstrips_k(e, k);
+            seg_range(e, k, reduce_every > 0, A, 0, e->d.h);
+        }
+    }
+    return MM_OK;
+}
+
+int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
+    MM_TRY(check_run(e, nsteps, reduce_every, "mm_run"));
+    if (nsteps == 0) return MM_OK;
     MM_TRY(set_device(e));
     // steps are numbered from the last fill / upload on, so a run split into several
     // calls reduces the same steps as one call
@@ -981,7 +1042,6 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     const long long entries =
         reduce_every > 0 ? (phase + nsteps) / reduce_every - phase / reduce_every : 0;
     MM_TRY(reserve_history(e, entries));
-    const int np = (int)e->passes.size();
     auto finish = [&]() {
         e->steps_done += nsteps;
         e->hist_host += entries;
@@ -991,19 +1051,11 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
         MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, true));
         return finish();
     }
-    // Replay a graph of `per` steps: a whole number of K-step passes, an even number of
-    // buffer flips (so the captured pointers are valid again) and of reduction periods
-    // (so the phase is the same at every replay).
-    const long long unit = steps_per_launch(e);
-    const long long flips = passk_ok(e) ? 1 : np;
-    long long len = unit * ((flips % 2) ? 2 : 1);
-    if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
-    if (len > 256 || nsteps < len || !e->graphs_ok) {
+    const long long per = graph_per(e, nsteps, reduce_every);
+    if (per == 0) {
         MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, false));
         return finish();
     }
-    long long per = len;
-    while (per < 16 && per * 2 <= nsteps) per *= 2;
     hipGraphExec_t g = nullptr;
     if (get_graph(e, per, reduce_every, phase, &g) != MM_OK) {
         // stream capture refused (e.g. by the RCCL build): run the same steps eagerly and

@@ -1,4 +1,14 @@
 // mm_passk_k2.hip -- instances of the K-step kernel (mm_passk.hpp) for K = 2.
+// Tuning (tools/libsweep.py --program c5, profiles/r02/libsweep_c5.log): the 3- and
+// 4-attribute instances fit two waves per SIMD (<= 256 registers) with one row of the
+// attributes prefetched; at the default 2 rows the 4-attribute K = 2 instance needs 257
+// registers, one wave per SIMD, and runs 1.7x slower.
+#ifndef MM_PASSK_MIN_WAVES
+#define MM_PASSK_MIN_WAVES 2
+#endif
+#ifndef MM_SEG_UN
+#define MM_SEG_UN 1
+#endif
 #include "mm_passk.hpp"
 
 namespace mm {
