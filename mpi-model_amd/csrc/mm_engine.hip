@@ -121,8 +121,9 @@ struct mm_engine {
 
     long long steps_done = 0;
 
-    // graph cache: key = (parity, length, reduce_every, reduction phase)
-    std::map<std::tuple<int, long long, long long, long long>, hipGraphExec_t> graphs;
+    // graph cache: key = (parity, length, reduce_every, reduction phase); value = the
+    // executable and whether one replay flips the ping-pong buffers
+    std::map<std::tuple<int, long long, long long, long long>, std::pair<hipGraphExec_t, int>> graphs;
 
     bool graphs_ok = true;      // MM_GRAPH=0 (or a refused capture) runs steps eagerly
     int graph_state = 0;        // 0 none yet, 1 replaying, -1 capture refused
@@ -147,7 +148,7 @@ int set_device(mm_engine* e) {
 }
 
 void drop_graphs(mm_engine* e) {
-    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.first);
     e->graphs.clear();
 }
 
@@ -500,9 +501,12 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
     if (passk_ok(e)) {
+        // ceil(n / K) passes of balanced length (20 steps at K = 8: 7 + 7 + 6, not
+        // 8 + 8 + 4): a pass costs about the same whatever its K, so fewer, even passes win
         const int kp = passk_steps(e);
         while (s < end) {
-            const int k = (int)std::min<long long>(kp, end - s);
+            const long long passes = (end - s + kp - 1) / kp;
+            const int k = (int)((end - s + passes - 1) / passes);
             int mask = 0;
             for (int j = 0; j < k; ++j)
                 if (red(s + j)) mask |= 1 << j;
@@ -530,11 +534,12 @@ long long gcd_ll(long long a, long long b) {
 }
 
 int get_graph(mm_engine* e, long long len, long long reduce_every, long long phase,
-              hipGraphExec_t* out) {
+              hipGraphExec_t* out, int* flip) {
     auto key = std::make_tuple(e->cur, len, reduce_every, phase);
     auto it = e->graphs.find(key);
     if (it != e->graphs.end()) {
-        *out = it->second;
+        *out = it->second.first;
+        *flip = it->second.second;
         return MM_OK;
     }
     const int cur0 = e->cur;
@@ -542,6 +547,7 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, long long pha
     const int rc = enqueue_steps(e, phase + 1, len, reduce_every, false);
     hipGraph_t g = nullptr;
     hipError_t ec = hipStreamEndCapture(e->s_comp, &g);
+    const int parity = e->cur ^ cur0;  // the captured passes' buffer flips, mod 2
     e->cur = cur0;  // capture only recorded the work; the state advances at replay
     e->comm_live = false;
     if (rc != MM_OK) {
@@ -553,9 +559,10 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, long long pha
     ec = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (ec != hipSuccess) return fail(MM_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ec));
-    e->graphs[key] = ge;
+    e->graphs[key] = std::make_pair(ge, parity);
     e->graph_count += 1;
     *out = ge;
+    *flip = parity;
     return MM_OK;
 }
 
@@ -979,6 +986,10 @@ long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every
     if (len > 256 || nsteps < len || !e->graphs_ok) return 0;
     long long per = len;
     while (per < 16 && per * 2 <= nsteps) per *= 2;
+    // a short run that is not a whole number of graphs becomes one graph (its passes
+    // balanced, enqueue_steps), instead of graphs plus an eager tail; keyed by the buffer
+    // parity like every graph, so an odd number of flips is fine
+    if (nsteps % per != 0 && nsteps <= 64 * unit) per = nsteps;
     return per;
 }
 
@@ -1009,12 +1020,15 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
     long long tail = nsteps;
     if (per > 0) {
         hipGraphExec_t g = nullptr;
-        if (get_graph(e, per, reduce_every, phase, &g) != MM_OK) {
+        int flip = 0;
+        if (get_graph(e, per, reduce_every, phase, &g, &flip) != MM_OK) {
             e->graph_note = g_last_error;
             (void)hipGetLastError();
             e->graphs_ok = false;
             e->graph_state = -1;
         } else {
+            MM_HIP(hipGraphUpload(g, e->s_comp));  // the first launch then uploads nothing
+            MM_HIP(hipStreamSynchronize(e->s_comp));
             tail = nsteps % per;
         }
     }
@@ -1057,7 +1071,8 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
         return finish();
     }
     hipGraphExec_t g = nullptr;
-    if (get_graph(e, per, reduce_every, phase, &g) != MM_OK) {
+    int flip = 0;
+    if (get_graph(e, per, reduce_every, phase, &g, &flip) != MM_OK) {
         // stream capture refused (e.g. by the RCCL build): run the same steps eagerly and
         // say so in mm_engine_info (graph_state -1, graph_note)
         e->graph_note = g_last_error;
@@ -1070,8 +1085,12 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     e->graph_state = 1;
     long long done = 0;
     for (; done + per <= nsteps; done += per) {
+        if (done > 0 && flip) {  // an odd graph replays at the other parity: its own graph
+            MM_TRY(get_graph(e, per, reduce_every, phase, &g, &flip));
+        }
         MM_HIP(hipGraphLaunch(g, e->s_comp));
         e->graph_launches += 1;
+        e->cur ^= flip;
     }
     if (done < nsteps)
         MM_TRY(enqueue_steps(e, phase + done + 1, nsteps - done, reduce_every, false));
