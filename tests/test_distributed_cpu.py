@@ -4,7 +4,7 @@ without GPUs.
 Each rank owns the slab mm_partition_rows gives it, keeps `depth` ghost rows above and
 below, and before every `depth` steps sends its first `depth` rows to rank-1 and its
 last `depth` rows to rank+1 -- the exchange the engine does with ncclSend/ncclRecv
-(mm_engine.hip halo_rccl; depth 2 for the fused two-step kernel). Steps are computed
+(mm_engine.hip halo_rccl; depth K for the K-step kernel, K <= 8). Steps are computed
 with the oracle on the slab; the gathered grid must equal the single-process oracle
 bit for bit (src/Model.hpp's row slabs, generalised to every cell and every step).
 """
@@ -94,6 +94,10 @@ def worker(rank, world, port, H, W, rate, steps, depth, out_q):
 
 @pytest.mark.parametrize("world,H,W,steps,depth", [
     (2, 37, 53, 5, 1), (2, 40, 29, 6, 2), (3, 41, 33, 7, 2), (3, 30, 20, 4, 1),
+    # the K-step kernel's depths (mm_engine.hip halo_depth): 3, 4 and 8 with ragged last
+    # passes, and slabs exactly as thin as the depth (the engine caps K by min slab rows)
+    (2, 40, 29, 9, 3), (3, 41, 33, 10, 4), (4, 16, 21, 9, 4), (2, 16, 19, 17, 8),
+    (3, 13, 17, 7, 4),
 ])
 def test_row_slabs_with_halo_exchange_bit_exact(O, world, H, W, steps, depth):
     ctx = tmp.get_context("spawn")
