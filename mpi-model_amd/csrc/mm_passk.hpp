@@ -113,6 +113,35 @@ __device__ __forceinline__ double dpp_upper(double src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// The same two shifts through the LDS crossbar (ds_bpermute_b32: no LDS memory, the DS
+// pipe instead of the VALU). A DPP shift of a double is two VALU moves, 4 of the 18 VALU
+// instructions of a level-row of two columns; ds_bpermute moves them to the otherwise idle
+// DS pipe. `addr` = 4 * source lane (wraps around the wave: the halo lanes get garbage
+// instead of 0, and their results are discarded either way).
+#ifndef MM_SHIFT_LDS
+#define MM_SHIFT_LDS 0
+#endif
+__device__ __forceinline__ double lds_shift(double src, int addr) {
+    const long long s = __double_as_longlong(src);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)s);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(s >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// A prefetched row is copied out of its ring slot where it is consumed (U rows after its
+// load was issued). Without the copy the slot's registers become the level's d = u - out
+// (v_fmac works in place), every reload lands in fresh registers, and the loop's back edge
+// copies them into the slots right after the last load -- a vmcnt(0) wait that exposes the
+// full memory latency once per U rows. The early clobber keeps the copy out of the slot.
+#ifndef MM_LOAD_COPY
+#define MM_LOAD_COPY 1
+#endif
+__device__ __forceinline__ double vcopy(double x) {
+    double y;
+    asm volatile("v_mov_b64 %0, %1" : "=&v"(y) : "v"(x));
+    return y;
+}
+
 // 1 + (i > 0) + (i < n-1) inside [0, n), 0 outside: cnt = span(x)*span(y) - 1
 __device__ __forceinline__ int span3k(long long n, long long i) {
     return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
@@ -172,6 +201,7 @@ struct Lane {
     int sy0, sy1;      // column spans of this lane's two columns
     bool fast_cols;    // all loaded columns interior
     bool own0, own1;   // this lane's columns are output cells of this wave
+    int from_lower, from_upper;  // ds_bpermute byte addresses of lanes i-1, i+1 (MM_SHIFT_LDS)
 };
 
 // Transfers of a chain, in declared order, on one cell's attribute values: out = r*u_a;
@@ -278,8 +308,13 @@ __device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, lon
         } else {
             const double p0 = w[a].sp0 + sn0[a], p1 = w[a].sp1 + sn1[a];
             const double c0 = p0 + w[a].sc0, c1 = p1 + w[a].sc1;
+#if MM_SHIFT_LDS
+            const double left = lds_shift(c1, c.from_lower);
+            const double right = lds_shift(c0, c.from_upper);
+#else
             const double left = dpp_lower(c1);   // c3 at column y0-1 (lane-1's second column)
             const double right = dpp_upper(c0);  // c3 at column y0+2 (lane+1's first column)
+#endif
             w0[a] = w[a].dc0 + ((left + c1) + p0);
             w1[a] = w[a].dc1 + ((c0 + right) + p1);
         }
@@ -402,10 +437,71 @@ __device__ __forceinline__ void passk_block(const PassArgs& A, const Lane& c, lo
     if (RED) write_sums<K, NA>(A, wid, lane, acc);
 }
 
+// Steady state of the SEGMENT schedule, iterations [b0, b1) (b0 = I0 mod U): every level
+// emits one row per iteration, level K's row rA + (i - I0) is stored. FAST: every row the
+// levels read in these iterations is an interior row of an interior strip.
+template <int K, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
+__device__ __forceinline__ void seg_steady(const PassArgs& A, const Lane& c, const Bufs<K, NA>& B,
+                                           int rA, int rB, unsigned voff, unsigned soff,
+                                           unsigned rowb, int b0, int b1, dv2 (&raw)[U][NA],
+                                           Win (&win)[K][NA], double (&pend0)[K][NA],
+                                           double (&pend1)[K][NA], double (&acc)[K][NA]) {
+    constexpr int I0 = 3 * K - 1;
+    for (int base = b0; base < b1; base += U) {
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int i = base + t;
+            const int slot = (I0 + t) % U;  // base = I0 (mod U)
+#pragma unroll
+            for (int j = K; j >= 1; --j) {
+                double u0[NA], u1[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    if (j == 1) {
+#if MM_LOAD_COPY
+                        u0[a] = vcopy(raw[slot][a].x);
+                        u1[a] = vcopy(raw[slot][a].y);
+#else
+                        u0[a] = raw[slot][a].x;
+                        u1[a] = raw[slot][a].y;
+#endif
+                        raw[slot][a] = load_row(B.in[a], voff + (unsigned)(i + U) * rowb);
+                    } else {
+                        u0[a] = pend0[j - 2][a];
+                        u1[a] = pend1[j - 2][a];
+                    }
+                }
+                const long long gx = c.gx0 + rA - K + i - 2 * (j - 1);
+                double w0[NA], w1[NA];
+                level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
+                const int r = rA - K - 2 * j + 1 + i;  // output row
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
+                    if (j == K) {
+                        store_row<NT>(B.out[a], soff + (unsigned)(i - I0) * rowb, w0[a], w1[a]);
+                    } else {
+                        pend0[j - 1][a] = w0[a];
+                        pend1[j - 1][a] = w1[a];
+                    }
+                }
+#if MM_LEVEL_BARRIER
+                // at most two levels in flight: bounds the live registers (occupancy)
+                if ((K - j) % MM_LEVEL_BARRIER == MM_LEVEL_BARRIER - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 // SEGMENT schedule: R = rB - rA rows (run time). Iterations 0 .. 3K-2 fill the levels
 // (compile-time); from iteration I0 = 3K-1 on every level emits, level K writes row
 // rA + (i - I0), and the loop runs R iterations (rounded up to U; the extra ones read
 // zeros past the input rows and their stores fall past the output rows).
+// A wave of an interior strip whose segment touches the grid's first or last rows runs
+// the general body only for the iterations that read those rows and the branch-free body
+// in between (the general body's per-row branches keep the K levels from interleaving).
 template <int K, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
 __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, long long wid,
                                               int lane, int rA, int rB, unsigned voff,
@@ -464,47 +560,28 @@ __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, 
         __builtin_amdgcn_sched_barrier(0);
     }
 
-    // steady state: every level emits one row per iteration
-    for (int base = I0; base < I0 + R; base += U) {
-#pragma unroll
-        for (int t = 0; t < U; ++t) {
-            const int i = base + t;
-            const int slot = (I0 + t) % U;  // base = I0 (mod U)
-#pragma unroll
-            for (int j = K; j >= 1; --j) {
-                double u0[NA], u1[NA];
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    if (j == 1) {
-                        u0[a] = raw[slot][a].x;
-                        u1[a] = raw[slot][a].y;
-                        raw[slot][a] = load_row(B.in[a], voff + (unsigned)(i + U) * rowb);
-                    } else {
-                        u0[a] = pend0[j - 2][a];
-                        u1[a] = pend1[j - 2][a];
-                    }
-                }
-                const long long gx = c.gx0 + rA - K + i - 2 * (j - 1);
-                double w0[NA], w1[NA];
-                level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-                const int r = rA - K - 2 * j + 1 + i;  // output row
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
-                    if (j == K) {
-                        store_row<NT>(B.out[a], soff + (unsigned)(i - I0) * rowb, w0[a], w1[a]);
-                    } else {
-                        pend0[j - 1][a] = w0[a];
-                        pend1[j - 1][a] = w1[a];
-                    }
-                }
-#if MM_LEVEL_BARRIER
-                // at most two levels in flight: bounds the live registers (occupancy)
-                if ((K - j) % MM_LEVEL_BARRIER == MM_LEVEL_BARRIER - 1) __builtin_amdgcn_sched_barrier(0);
-#endif
-            }
-            __builtin_amdgcn_sched_barrier(0);
+    const int end = I0 + (R + U - 1) / U * U;
+    if (FAST) {
+        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, I0, end,
+                                                   raw, win, pend0, pend1, acc);
+    } else {
+        int f0 = end, f1 = end;  // iterations [f0, f1) read interior rows only
+        if (c.fast_cols) {
+            // iteration i: the levels read global rows g - 2(K-1) .. g, g = gx0 + rA - K + i
+            const long long g0 = c.gx0 + rA - K;
+            const long long lo = 1 + 2 * (K - 1) - g0;  // first i with every row >= 1
+            const long long hi = c.H - 1 - g0;          // first i with a row > H-2
+            const long long a0 = lo <= I0 ? I0 : I0 + (lo - I0 + U - 1) / U * U;
+            const long long a1 = hi <= I0 ? I0 : I0 + (hi - I0) / U * U;
+            f0 = (int)min((long long)end, a0);
+            f1 = (int)max((long long)f0, min((long long)end, a1));
         }
+        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, I0, f0,
+                                                    raw, win, pend0, pend1, acc);
+        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, f0, f1,
+                                                   raw, win, pend0, pend1, acc);
+        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, f1, end,
+                                                    raw, win, pend0, pend1, acc);
     }
     if (RED) write_sums<K, NA>(A, wid, lane, acc);
 }
@@ -596,6 +673,8 @@ __global__ __launch_bounds__(kBlock, MM_PASSK_MIN_WAVES) void mm_passk_kernel(co
     c.fast_cols = c0 >= 1 && c0 + kStripCols <= W - 1;  // loaded cols in [1, W-2]
     c.own0 = store_lane;
     c.own1 = store_lane && y0 + 1 < W;
+    c.from_lower = ((lane + 63) & 63) * 4;
+    c.from_upper = ((lane + 1) & 63) * 4;
 
     // a wave whose input rows and loaded columns are all interior (cnt == 8 everywhere)
     // runs the branch-free body; edge waves run the general one

@@ -4,7 +4,17 @@ demangled-ish name, VGPRs, AGPRs, SGPRs, scratch, occupancy (waves per SIMD), LD
 import re
 import sys
 
-KEYS = ("VGPRs", "AGPRs", "TotalSGPRs", "ScratchSize", "Occupancy", "LDS Size")
+KEYS = ("VGPRs", "AGPRs", "VGPRs Spill", "SGPRs Spill", "TotalSGPRs", "ScratchSize", "Occupancy",
+        "LDS Size")
+
+
+def demangle(name):
+    try:
+        import subprocess
+        return subprocess.run(["c++filt", name], capture_output=True, text=True,
+                              timeout=10).stdout.strip().replace("mm::(anonymous namespace)::", "")
+    except (OSError, subprocess.SubprocessError):
+        return name
 
 
 def main(path):
@@ -19,11 +29,11 @@ def main(path):
         if cur is None:
             continue
         for k in KEYS:
-            m = re.search(r"\s%s(?: \[bytes/lane\])?: (\d+)" % re.escape(k), ln)
+            m = re.search(r"\s%s(?: \[[^\]]*\])?: (\d+)" % re.escape(k), ln)
             if m:
                 cur[k] = int(m.group(1))
     for r in rows:
-        print(r["name"], " ".join(f"{k.split()[0]}={r.get(k)}" for k in KEYS))
+        print(demangle(r["name"]), " ".join(f"{k.replace(' ', '')}={r.get(k)}" for k in KEYS))
 
 
 if __name__ == "__main__":
