@@ -102,7 +102,7 @@ struct mm_engine {
     bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
     int kpass = 0;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps; 0: auto)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
-    double seg_waves = 2.0;  // segment waves per resident wave slot (MM_SEG_WAVES)
+    double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
     double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
     int ncu = 0;             // compute units of the device
@@ -389,22 +389,34 @@ long long seg_wave_count(long long n, long long ns, long long r, long long re) {
 // Segment plan of rows [lo, hi) of a k-step pass: r rows per interior-strip segment, re
 // per edge-strip segment (seg_edge x r: the edge strips run the slower general body),
 // the smallest r for which every wave fits seg_waves x the chip's resident wave slots
-// (the kernel's occupancy x CUs), so one launch is one wave generation.
+// (the kernel's occupancy x CUs). Auto: 4 waves per slot while segments stay >= 256 rows
+// (large slabs: the waves that finish last are shorter), else 2 (short segments pay 2K
+// extra input rows each) -- profiles/r02b/segwaves: 32768^2 K = 7/8 and 16384^2 K = 6..8
+// run 3-5 % faster at 4 than at 2, 4096^2 K = 7 12 % slower.
 void seg_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
     const int nt = e->variant & 1;
     int& wpc = e->wpc[red ? 1 : 0][nt][e->na][k];
     if (!wpc) wpc = std::max(1, mm::passk_waves_per_cu(k, e->na, red, nt));
-    const long long want = std::max<long long>(1, (long long)(e->seg_waves * e->ncu * wpc));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double units = ns < 3 ? (double)ns / e->seg_edge : (double)(ns - 2) + 2.0 / e->seg_edge;
-    long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
-    r = std::min(std::max<long long>(r, 16), maxr);
     auto re_of = [&](long long rr) {
         return std::min(maxr, std::max<long long>(8, (long long)((double)rr * e->seg_edge)));
     };
-    while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
-    r = std::min(r, maxr);
+    auto plan = [&](double sw) {
+        const long long want = std::max<long long>(1, (long long)(sw * e->ncu * wpc));
+        long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
+        r = std::min(std::max<long long>(r, 16), maxr);
+        while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
+        return std::min(r, maxr);
+    };
+    long long r;
+    if (e->seg_waves > 0.0) {
+        r = plan(e->seg_waves);
+    } else {
+        r = plan(4.0);
+        if (r < 256) r = plan(2.0);
+    }
     A.seg = 1;
     A.th = (int)r;
     A.th_edge = (int)re_of(r);
@@ -581,10 +593,13 @@ int choose_th(const mm_engine* e) {
 int ensure_partials(mm_engine* e) {
     // doubles: one-step kernel, 128-column strips x 8-row blocks with kMaxAttr sums per
     // wave (+ 1-row border blocks); mm_passk_kernel, segments of >= 8 rows (edge strips)
-    // plus 4-row border blocks with K x NA <= 8 sums per wave
+    // plus 4-row border blocks (depth <= kGhost rows on each side) with K x NA sums per
+    // wave: K <= kMaxSteps for one attribute, K <= 2 for up to kMaxAttr
     long long need = (waves_for(e, e->d.h, 8) + 2 * waves_for(e, 2, 1) + 16) * mm::kMaxAttr;
     const long long ns = nstrips_k(e, mm::kMaxSteps);
-    need = std::max(need, (ns * ((e->d.h + 7) / 8 + 4) + 16) * 8);
+    const long long border = 2 * ((mm::kGhost + mm::kBorderRows - 1) / mm::kBorderRows) + 2;
+    need = std::max(need, (ns * ((e->d.h + 7) / 8 + border) + 16) *
+                              std::max(mm::kMaxSteps, 2 * mm::kMaxAttr));
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;

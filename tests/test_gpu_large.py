@@ -70,3 +70,28 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
         for b, got in mirror_src.items():
             flipped = e.read_rows(b, 64)
             assert np.array_equal(flipped, got[::-1, ::-1]), (N, b)
+
+
+
+def test_driver_length_run_balanced_passes(gpu, O):
+    """The driver's 20-step run on a 16384^2 grid: three balanced K-step passes (7 + 7 + 6,
+    mm_engine.hip enqueue_steps), equal to 20 single steps bit for bit on three bands
+    widened by the 20-row cone, total conserved."""
+    H = W = 16384
+    steps = 20
+    with gpu.Engine(H, W) as e:
+        e.fill_random(0)
+        s0 = e.sums()[0]
+        e.add_diffuse(0, RATE)
+        e.set_timing(True)
+        e.run(steps)
+        n_launch, _, _ = e.timing()
+        e.set_timing(False)
+        assert n_launch == 3
+        s1 = e.sums()[0]
+        bands = {b: e.read_rows(b, 64) for b in (0, H // 2 - 32, H - 64)}
+    assert abs(s1 - s0) <= 1e-12 * s0
+    for b, got in bands.items():
+        lo, hi = max(0, b - steps), min(H, b + 64 + steps)
+        want = band_oracle(O, H, W, lo, hi, steps, RATE)[b - lo:b - lo + 64]
+        assert np.array_equal(got, want), (b, int(np.count_nonzero(got != want)))

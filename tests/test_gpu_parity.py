@@ -223,7 +223,7 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
 
 @pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 3}, {"MM_STEPS_PER_PASS": 2},
                                  {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
-                                 {"MM_PASSK": 0}], ids=env_id)
+                                 {"MM_STEPS_PER_PASS": 7}, {"MM_PASSK": 0}], ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
     H, W, steps = 130, 257, 12
@@ -247,7 +247,7 @@ def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
         assert abs(a - b) <= 1e-12 * b
 
 
-@pytest.mark.parametrize("k", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("k", [2, 3, 4, 6, 7, 8])
 def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k):
     # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
     # multiple of the graph length, so the tail runs eagerly
@@ -364,7 +364,7 @@ def test_engine_rejects_bad_shapes(gpu):
             e.point_apply(8, 0, 1.0, 0.1)
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 6, 7, 8])
 @pytest.mark.parametrize("graph", [0, 1])
 def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     # The RCCL halo path on one GPU: one rank whose two neighbours are itself

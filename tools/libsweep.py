@@ -27,7 +27,7 @@ def child(a):
     mm.LIB_PATH = a.lib
     mm.lib()
     import oracle as O
-    os.environ.update(json.loads(a.env))
+    os.environ.update({k: str(v) for k, v in json.loads(a.env).items()})
     out = {}
     # correctness: 9 steps (K-step passes + a shorter tail) against the oracle
     H, W = 301, 1000
