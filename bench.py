@@ -244,14 +244,17 @@ def main():
         el = float(t.item())
     s_after = global_total(eng)
 
-    # kernel pass: whole K-step passes (at least 3, about the timed steps), each step
-    # kernel bracketed by HIP events on its stream -- the launches rocprofv3 averages
-    spl0 = eng.info()["steps_per_launch"]
-    timing_steps = spl0 * max(3, -(-args.steps // spl0))
+    # kernel pass: the timed run's own passes (mm_pass_plan), repeated eagerly until at
+    # least 3 launches, each step kernel bracketed by HIP events on its stream -- the
+    # launches rocprofv3 averages
+    plan = eng.pass_plan(args.steps)
+    reps = max(1, -(-3 // max(len(plan), 1)))
     eng.set_timing(True)
-    eng.run(timing_steps, reduce_every)
+    for _ in range(reps):
+        eng.run(args.steps, reduce_every)
     n_launch, kern_ms, bytes_per_launch = eng.timing()
     eng.set_timing(False)
+    timing_steps = reps * args.steps
     info = eng.info()
     if info["graph_state"] == 1:
         path = f"hipGraph replay ({info['graph_launches']} graph launches)"
@@ -265,7 +268,7 @@ def main():
     if rank == 0:
         kern_avg_ms = kern_ms / max(n_launch, 1)
         launches_per_step = n_launch / max(timing_steps, 1)
-        spl = info["steps_per_launch"]
+        spl = max(plan) if info["kernel"] == 2 else 1  # steps of the dominant (longest) pass
         kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel"}[info["kernel"]]
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         traffic = None
@@ -273,9 +276,9 @@ def main():
         if os.path.exists(tf):  # only when it was measured on this kernel
             with open(tf) as f:
                 pmc = json.load(f)
-            if kname in pmc.get(f"{args.workload}_n{N}_kernel", "") and \
-                    pmc.get(f"{args.workload}_n{N}_steps_per_launch", spl) == spl:
-                traffic = pmc.get(f"{args.workload}_n{N}_bytes_per_launch")
+            key = f"{args.workload}_n{N}_k{spl}"
+            if kname in pmc.get(f"{key}_kernel", ""):
+                traffic = pmc.get(f"{key}_bytes_per_launch")
         cons = abs(s_after - s_before) / abs(s_before)
         line = {
             "metric": "cell-updates/s (GCUPS) per step + % of HBM roofline",
@@ -292,7 +295,9 @@ def main():
             "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
                     "seed 0x4D50494D, generated on the device",
             "config": {"workload": f"{args.workload}: {wl['desc']}", "grid": [H, W],
-                       "path": f"{path}, {kname}, {spl} fused step(s) per kernel pass",
+                       "path": f"{path}, {kname}, {len(plan)} pass(es) of "
+                               f"{'+'.join(map(str, plan)) if len(plan) <= 8 else f'{spl} (x{len(plan)})'}"
+                               f" fused steps",
                        "rows_per_gpu": h, "n_attr": na, "rate": RATE,
                        "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else "")
                        + (" (self-halo: RCCL exchange with itself)" if args.self_halo else ""),
@@ -308,7 +313,7 @@ def main():
                 "kernel": kname,
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
-                "steps_per_launch": info["steps_per_launch"],
+                "steps_per_launch": spl,
                 "launches_per_step": launches_per_step,
                 # BASELINE.md's formula: GCUPS x 16 B x A / 8 TB/s (per GPU); above 1.0
                 # when K steps share one HBM round trip (temporal blocking)

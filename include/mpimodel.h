@@ -165,13 +165,14 @@ int mm_device_synchronize(int device);
 /* ---- engine ------------------------------------------------------------- */
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
  * init loop (src/Model.hpp:154-157): device buffers are (h + 2*kGhost) x pitch fp64 per
- * attribute (kGhost = 8 ghost rows above and below, the deepest K-step pass), two of
+ * attribute (kGhost = 10 ghost rows above and below, the deepest K-step pass), two of
  * them (Jacobi ping-pong).
  * With nranks > 1 the steps per kernel pass (and so the halo depth) are capped by the
  * thinnest slab of the chain: RCCL engines all-reduce it at creation; host-transport
  * engines assume mm_partition_rows slabs (floor(H/nranks) rows at least).
  * Environment: MM_PASSK=0 (or MM_FUSE=0) runs one step per kernel pass, MM_GRAPH=0
- * disables the hipGraph replay, MM_STEPS_PER_PASS (1..8; fixes K), MM_ROWS_PER_WAVE (8/16/32),
+ * disables the hipGraph replay, MM_STEPS_PER_PASS (1..10; fixes K), MM_PASS_PLAN=0
+ * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
  * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal policy)
  * override tuning; MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
@@ -217,6 +218,11 @@ int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
  * instantiate its hipGraph, plan its eager tail passes (loading their kernels) -- without
  * running any step. Optional: mm_run does the same work on first use. */
 int mm_prepare(mm_engine* eng, long long nsteps, long long reduce_every);
+/* The kernel passes mm_run(eng, nsteps, .) launches: *count passes, the steps of the first
+ * min(*count, cap) in lens[] (K-step passes; 1 per step for the one-step kernel). Host-only
+ * planning, no device work. Replaces nothing in the reference: its time loop
+ * (src/Model.hpp:180-183) is commented out. */
+int mm_pass_plan(mm_engine* eng, long long nsteps, int* lens, int cap, int* count);
 int mm_synchronize(mm_engine* eng);
 
 /* Sums of the owned cells. mm_sums reduces the CURRENT state now (synchronous).

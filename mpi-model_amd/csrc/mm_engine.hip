@@ -102,8 +102,9 @@ struct mm_engine {
     bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
     int kpass = 0;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps; 0: auto)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
+    bool plan = true;        // pass-length planner (MM_PASS_PLAN=0: balanced passes of K)
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
-    double seg_edge = 0.5;   // edge-strip segment length / interior length (MM_SEG_EDGE)
+    double seg_edge = 0.0;   // edge-strip segment length / interior length (MM_SEG_EDGE; 0: auto)
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
@@ -386,6 +387,15 @@ long long seg_wave_count(long long n, long long ns, long long r, long long re) {
     return 2 * ((n + re - 1) / re) + (ns - 2) * ((n + r - 1) / r);
 }
 
+// Edge-strip segment length / interior segment length of a k-step pass. The two edge
+// strips run the general body, several times slower per row than the branch-free one,
+// and at K >= 9 it spills; their segments are cut shorter so they end with the rest
+// (profiles/r02b/k9k10/edge_*: K = 10 at 0.5 takes 1.5x the pass time of 0.1).
+double seg_edge_of(const mm_engine* e, int k) {
+    if (e->seg_edge > 0.0) return e->seg_edge;
+    return k >= 10 ? 0.1 : (k == 9 ? 0.2 : 0.5);
+}
+
 // Segment plan of rows [lo, hi) of a k-step pass: r rows per interior-strip segment, re
 // per edge-strip segment (seg_edge x r: the edge strips run the slower general body),
 // the smallest r for which every wave fits seg_waves x the chip's resident wave slots
@@ -399,9 +409,10 @@ void seg_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lon
     if (!wpc) wpc = std::max(1, mm::passk_waves_per_cu(k, e->na, red, nt));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
-    const double units = ns < 3 ? (double)ns / e->seg_edge : (double)(ns - 2) + 2.0 / e->seg_edge;
+    const double edge = seg_edge_of(e, k);
+    const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
     auto re_of = [&](long long rr) {
-        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * e->seg_edge)));
+        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
     };
     auto plan = [&](double sw) {
         const long long want = std::max<long long>(1, (long long)(sw * e->ncu * wpc));
@@ -506,6 +517,46 @@ int steps_per_launch(const mm_engine* e) { return passk_ok(e) ? passk_steps(e) :
 // Ghost rows one exchange must fill (host transport: mm_halo_export_rows / _import_rows).
 int halo_depth(const mm_engine* e) { return steps_per_launch(e); }
 
+// Modelled time of one K-step pass of a large one-attribute slab, relative to the K = 8
+// pass: the HBM stream of the grid (`kStream`: the K <= 7 passes, which the stream
+// bounds), or the VALU work of K levels over the strips' 128 - 4*ceil(K/2) output
+// columns, whichever is longer (K >= 8 are VALU-bound: 32768^2 on one box, K = 8 / 9 /
+// 10: 3437 / 3884 / 4326 us, profiles/r02b/k9k10/edge_*; K = 7 0.93 of K = 8,
+// profiles/r02b/segwaves).
+double pass_cost(int k) {
+    constexpr double kStream = 0.93;
+    constexpr double kValuPerLevel = 112.0 / (8.0 * 128.0);  // K = 8 -> 1.0
+    const double useful = (double)mm::passk_out_cols(k) / (double)mm::kStripCols;
+    return std::max(kStream, kValuPerLevel * (double)k / useful);
+}
+
+// Steps of the next K-step pass when n steps remain: ceil(n / K) passes of balanced
+// length (20 steps at K = 8: 7 + 7 + 6, not 8 + 8 + 4), where K is the auto or configured
+// steps per pass. On a large one-attribute slab with K auto, the planner also considers
+// fewer, longer passes (up to kMaxSteps, capped by the chain's thinnest slab) and takes
+// the plan of least modelled time: 20 steps run as 10 + 10, a long run stays at K = 8
+// (1000 steps: 125 passes).
+int next_pass_len(const mm_engine* e, long long n) {
+    const int kp = passk_steps(e);
+    long long best_p = (n + kp - 1) / kp;
+    const bool big = (double)e->d.h * (double)e->d.W >= 268435456.0;
+    if (e->plan && e->kpass == 0 && e->na == 1 && big && n > kp) {
+        long long kx = mm::passk_max_steps(1);
+        if (e->d.nranks > 1) kx = std::min<long long>(kx, e->min_rows);
+        double best = 1e300;
+        const long long p_max = best_p;
+        for (long long p = (n + kx - 1) / kx; p <= p_max; ++p) {
+            const long long q = n / p, r = n % p;  // r passes of q + 1 steps, p - r of q
+            const double t = (double)r * pass_cost((int)q + 1) + (double)(p - r) * pass_cost((int)q);
+            if (t < best * (1.0 - 1e-9)) {
+                best = t;
+                best_p = p;
+            }
+        }
+    }
+    return (int)((n + best_p - 1) / best_p);
+}
+
 // Enqueue steps [first, first+n) of a run (1-based step numbers decide the reductions).
 int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_every,
                   bool time_it) {
@@ -513,12 +564,8 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
     if (passk_ok(e)) {
-        // ceil(n / K) passes of balanced length (20 steps at K = 8: 7 + 7 + 6, not
-        // 8 + 8 + 4): a pass costs about the same whatever its K, so fewer, even passes win
-        const int kp = passk_steps(e);
         while (s < end) {
-            const long long passes = (end - s + kp - 1) / kp;
-            const int k = (int)((end - s + passes - 1) / passes);
+            const int k = next_pass_len(e, end - s);
             int mask = 0;
             for (int j = 0; j < k; ++j)
                 if (red(s + j)) mask |= 1 << j;
@@ -748,6 +795,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         if (v >= 1 && v <= mm::kMaxSteps) e->kpass = v;
         if (v >= 1) e->kpass_multi = std::min(v, 2);
     }
+    if (const char* p = std::getenv("MM_PASS_PLAN")) e->plan = std::atoi(p) != 0;
     if (const char* f = std::getenv("MM_SEG_WAVES")) {
         const double v = std::atof(f);
         if (v > 0.0) e->seg_waves = v;
@@ -1049,15 +1097,32 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
     }
     // the eagerly launched passes: plan them now, which loads their kernels' code objects
     if (passk_ok(e) && tail > 0) {
-        const int kp = passk_steps(e);
-        for (long long s = 0; s < tail; s += kp) {
-            const int k = (int)std::min<long long>(kp, tail - s);
+        for (long long s = 0, k = 0; s < tail; s += k) {
+            k = next_pass_len(e, tail - s);
             mm::PassArgs A;
             std::memset(&A, 0, sizeof A);
-            A.nstrips = (int)nstrips_k(e, k);
-            seg_range(e, k, reduce_every > 0, A, 0, e->d.h);
+            A.nstrips = (int)nstrips_k(e, (int)k);
+            seg_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
         }
     }
+    return MM_OK;
+}
+
+int mm_pass_plan(mm_engine* e, long long nsteps, int* lens, int cap, int* count) {
+    if (!e || nsteps < 0 || cap < 0 || (cap > 0 && !lens) || !count)
+        return fail(MM_ERR_INVALID, "mm_pass_plan: bad arguments");
+    if (e->passes.empty()) return fail(MM_ERR_STATE, "mm_pass_plan: no flow added (mm_add_flow)");
+    int n = 0;
+    if (passk_ok(e)) {
+        for (long long s = 0, k = 0; s < nsteps; s += k, ++n) {
+            k = next_pass_len(e, nsteps - s);
+            if (n < cap) lens[n] = (int)k;
+        }
+    } else {
+        for (long long s = 0; s < nsteps; ++s, ++n)
+            if (n < cap) lens[n] = 1;
+    }
+    *count = n;
     return MM_OK;
 }
 

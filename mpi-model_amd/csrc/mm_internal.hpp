@@ -11,7 +11,7 @@ constexpr int kMaxChain = 8;    // elementwise transfers before / after a pass's
 constexpr int kStripCols = 128; // columns per wave: 64 lanes x double2 (16 B per lane)
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
-constexpr int kMaxSteps = 8;    // fused steps per pass of mm_passk_kernel (one attribute)
+constexpr int kMaxSteps = 10;    // fused steps per pass of mm_passk_kernel (one attribute)
 constexpr int kGhost = kMaxSteps;  // ghost rows above and below a slab (K fused steps need K)
 constexpr int kBorderRows = 4;     // rows per wave of the K-step kernel's border launches
 

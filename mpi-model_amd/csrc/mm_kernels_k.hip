@@ -1,5 +1,5 @@
 // mm_kernels_k.hip -- dispatch of the K-step kernel (templates: mm_passk.hpp, instances:
-// mm_passk_k1..4.hip) and the fixed-order level-sum finalize kernel.
+// mm_passk_k1..10.hip) and the fixed-order level-sum finalize kernel.
 #include "mm_passk.hpp"
 
 namespace mm {
@@ -67,6 +67,8 @@ int passk_waves_per_cu(int k, int na, bool red, int nt) {
         case 6: return passk_waves_k6(na, red, nt);
         case 7: return passk_waves_k7(na, red, nt);
         case 8: return passk_waves_k8(na, red, nt);
+        case 9: return passk_waves_k9(na, red, nt);
+        case 10: return passk_waves_k10(na, red, nt);
         default: return 0;
     }
 }
@@ -82,6 +84,8 @@ hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t 
         case 6: return passk_launch_k6(na, red, a, s, variant);
         case 7: return passk_launch_k7(na, red, a, s, variant);
         case 8: return passk_launch_k8(na, red, a, s, variant);
+        case 9: return passk_launch_k9(na, red, a, s, variant);
+        case 10: return passk_launch_k10(na, red, a, s, variant);
         default: return hipErrorInvalidValue;
     }
 }

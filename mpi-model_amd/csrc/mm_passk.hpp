@@ -64,6 +64,8 @@ MM_PASSK_DECL(5)
 MM_PASSK_DECL(6)
 MM_PASSK_DECL(7)
 MM_PASSK_DECL(8)
+MM_PASSK_DECL(9)
+MM_PASSK_DECL(10)
 #undef MM_PASSK_DECL
 
 namespace {

@@ -29,7 +29,7 @@ EXPORTS = [
     "mm_owner_reference", "mm_partition_rows", "mm_neighbor_count", "mm_comm_id_size",
     "mm_comm_id_create", "mm_device_count", "mm_device_synchronize", "mm_engine_create", "mm_engine_destroy",
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
-    "mm_point_apply", "mm_run", "mm_prepare", "mm_synchronize", "mm_sums", "mm_sums_history",
+    "mm_point_apply", "mm_run", "mm_prepare", "mm_pass_plan", "mm_synchronize", "mm_sums", "mm_sums_history",
     "mm_clear_history", "mm_halo_export_rows", "mm_halo_import_rows", "mm_halo_export",
     "mm_halo_import", "mm_debug_read_rows",
     "mm_set_timing", "mm_timing", "mm_partition_rect_reference", "mm_owner_rect_reference",
@@ -101,6 +101,7 @@ def lib():
             "mm_point_apply": (I, [P, I, LL, LL, D, D]),
             "mm_run": (I, [P, LL, LL]),
             "mm_prepare": (I, [P, LL, LL]),
+            "mm_pass_plan": (I, [P, LL, pI, I, pI]),
             "mm_synchronize": (I, [P]),
             "mm_sums": (I, [P, P]),
             "mm_sums_history": (I, [P, P, LL, pLL]),
@@ -305,6 +306,14 @@ class Engine:
     def prepare(self, nsteps, reduce_every=0):
         """Capture / plan what run(nsteps, reduce_every) will launch, running no step."""
         check(lib().mm_prepare(self.ptr, nsteps, reduce_every))
+
+    def pass_plan(self, nsteps):
+        """Steps of each kernel pass run(nsteps) launches (mm_pass_plan)."""
+        cnt = ctypes.c_int()
+        check(lib().mm_pass_plan(self.ptr, nsteps, None, 0, ctypes.byref(cnt)))
+        buf = (ctypes.c_int * max(cnt.value, 1))()
+        check(lib().mm_pass_plan(self.ptr, nsteps, buf, cnt.value, ctypes.byref(cnt)))
+        return list(buf[:cnt.value])
 
     def synchronize(self):
         check(lib().mm_synchronize(self.ptr))

@@ -12,8 +12,8 @@ mkdir -p $OUT
 set -o pipefail
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace rc=$?"; tail -20 $OUT/trace.log; exit 3; }
 echo trace ok
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS --steps 32 > $OUT/fetch.log 2>&1 || { echo "fetch rc=$?"; tail -20 $OUT/fetch.log; exit 3; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS --steps ${PMCSTEPS:-32} > $OUT/fetch.log 2>&1 || { echo "fetch rc=$?"; tail -20 $OUT/fetch.log; exit 3; }
 echo fetch ok
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS --steps 32 > $OUT/write.log 2>&1 || { echo "write rc=$?"; tail -20 $OUT/write.log; exit 3; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS --steps ${PMCSTEPS:-32} > $OUT/write.log 2>&1 || { echo "write rc=$?"; tail -20 $OUT/write.log; exit 3; }
 echo write ok
 python3 tools/prof_summary.py $OUT $WL > $OUT/summary.json && cat $OUT/summary.json

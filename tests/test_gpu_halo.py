@@ -66,7 +66,7 @@ CHAINS = [(64, 300, 2), (37, 130, 3), (27, 257, 3), (100, 488, 3), (41, 200, 8),
           (24, 257, 8), (16, 130, 8), (9, 124, 8), (300, 700, 2)]
 
 
-@pytest.mark.parametrize("k", [8, 7, 6, 5, 4, 3, 2, 1])
+@pytest.mark.parametrize("k", [10, 9, 8, 7, 6, 5, 4, 3, 2, 1])
 @pytest.mark.parametrize("H,W,G", CHAINS)
 def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k):
     engines = make_chain(gpu, monkeypatch, H, W, G, env={"MM_STEPS_PER_PASS": k})
@@ -178,7 +178,7 @@ def test_host_halo_rejects_more_steps_than_depth(gpu, monkeypatch):
         with pytest.raises(gpu.MMError):
             e.run(d + 1)
         with pytest.raises(gpu.MMError):
-            e.halo_export(9)  # more rows than the ghost zone (kGhost = 8) holds
+            e.halo_export(11)  # more rows than the ghost zone (kGhost = 10) holds
     finally:
         close(engines)
 

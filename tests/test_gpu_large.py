@@ -73,10 +73,31 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
 
 
 
-def test_driver_length_run_balanced_passes(gpu, O):
-    """The driver's 20-step run on a 16384^2 grid: three balanced K-step passes (7 + 7 + 6,
-    mm_engine.hip enqueue_steps), equal to 20 single steps bit for bit on three bands
-    widened by the 20-row cone, total conserved."""
+
+def test_pass_planner_plans(gpu, monkeypatch):
+    """mm_pass_plan on a 16384^2 slab: short runs take fewer, deeper passes (20 steps:
+    10 + 10), long runs stay at K = 8; MM_PASS_PLAN=0 / a fixed K give balanced passes."""
+    with gpu.Engine(16384, 16384) as e:
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [10, 10]
+        assert e.pass_plan(16) == [8, 8]
+        assert e.pass_plan(9) == [9]
+        assert e.pass_plan(1000) == [8] * 125
+        assert e.pass_plan(0) == []
+    monkeypatch.setenv("MM_PASS_PLAN", "0")
+    with gpu.Engine(16384, 16384) as e:
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [7, 7, 6]
+    monkeypatch.delenv("MM_PASS_PLAN")
+    with gpu.Engine(4096, 4096) as e:  # small slab: K = 7, no planner
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [7, 7, 6]
+
+
+def test_driver_length_run_two_deep_passes(gpu, O):
+    """The driver's 20-step run on a 16384^2 grid: two K = 10 passes (the planner),
+    equal to 20 single steps bit for bit on three bands widened by the 20-row cone (top
+    edge, middle, bottom edge: every column, so both edge strips), total conserved."""
     H = W = 16384
     steps = 20
     with gpu.Engine(H, W) as e:
@@ -87,7 +108,7 @@ def test_driver_length_run_balanced_passes(gpu, O):
         e.run(steps)
         n_launch, _, _ = e.timing()
         e.set_timing(False)
-        assert n_launch == 3
+        assert n_launch == 2
         s1 = e.sums()[0]
         bands = {b: e.read_rows(b, 64) for b in (0, H // 2 - 32, H - 64)}
     assert abs(s1 - s0) <= 1e-12 * s0

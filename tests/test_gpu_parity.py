@@ -187,7 +187,7 @@ def make_env_engine(gpu, monkeypatch, H, W, n_attr=1, **env):
 # every way the engine can run a single-diffusion program: one step per pass, and the
 # K-step overlapped-strip kernel at each K / row block / block order
 FUSE_ENVS = [{"MM_PASSK": 0}, {}] + [
-    {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 5, 6, 7, 8)
+    {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 5, 6, 7, 8, 9, 10)
 ] + [{"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0},
      {"MM_XCD_REMAP": 1}, {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16}]
 
@@ -223,7 +223,8 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
 
 @pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 3}, {"MM_STEPS_PER_PASS": 2},
                                  {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
-                                 {"MM_STEPS_PER_PASS": 7}, {"MM_PASSK": 0}], ids=env_id)
+                                 {"MM_STEPS_PER_PASS": 7},
+                                 {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}], ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
     H, W, steps = 130, 257, 12
@@ -247,11 +248,12 @@ def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
         assert abs(a - b) <= 1e-12 * b
 
 
-@pytest.mark.parametrize("k", [2, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("k", [2, 3, 4, 6, 7, 8, 9, 10])
 def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k):
     # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
-    # multiple of the graph length, so the tail runs eagerly
-    H, W, steps = 300, 700, 50
+    # multiple of the graph length, so the tail runs eagerly (K = 10: a graph holds 60
+    # steps -- an even number of flips and whole reduction periods -- so run 130)
+    H, W, steps = 300, 700, (50 if k < 10 else 130)
     e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k)
     e.fill_random(0)
     e.add_diffuse(0, 0.2)
@@ -364,7 +366,7 @@ def test_engine_rejects_bad_shapes(gpu):
             e.point_apply(8, 0, 1.0, 0.1)
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("graph", [0, 1])
 def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     # The RCCL halo path on one GPU: one rank whose two neighbours are itself
