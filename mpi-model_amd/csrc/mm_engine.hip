@@ -502,10 +502,11 @@ bool passk_ok(const mm_engine* e) {
 // Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
 // past the thinnest slab of the chain (every rank sends K owned rows each way).
 int passk_steps(const mm_engine* e) {
-    // one attribute, auto: K = 8 on slabs of >= 2^28 cells, else 7 -- the fastest K of
-    // the round-2 sweeps (profiles/r02/sweep_k_*.log: 32768^2 and 16384^2 favour 8, 4096^2
+    // one attribute, auto: K = 8 on slabs of >= 2^27 cells, else 7 -- the fastest K per
+    // step of the round-2 sweeps (profiles/r02/sweep_k_*.log, profiles/r02c/sweep_*x32768:
+    // 32768^2, 16384^2 and the 8192- and 4096-row slabs of 32768 columns favour 8, 4096^2
     // with its short segments 7; K <= 4 leaves the VALU idle behind the HBM stream)
-    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->d.h * (double)e->d.W >= 268435456.0 ? 8 : 7);
+    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->d.h * (double)e->d.W >= 134217728.0 ? 8 : 7);
     int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
     if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
     return std::max(1, k);
