@@ -1097,8 +1097,9 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
         }
     }
     // every K-step kernel instance the run launches: one empty launch each, so the first
-    // timed pass does not bind its code object (a cold K = 10 pass cost ~0.4 ms,
-    // profiles/r02c/gap.log)
+    // pass of the run does not bind its code object. (The ~0.3 ms a 20-step run loses after
+    // a 5-step warmup against a 20-step one is not this, nor the graph: eager launches
+    // lose it too -- profiles/r02c/gap/.)
     if (passk_ok(e)) {
         bool seen[mm::kMaxSteps + 1] = {};
         for (long long s = 0, k = 0; s < nsteps; s += k) {
