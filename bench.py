@@ -321,6 +321,20 @@ def main():
             },
             "check": {"total_rel_drift": cons},
         }
+        if info["kernel"] == 2 and na == 1 and kern_ms > 0:
+            # the K-step kernel's other roof: its steady-state loop issues
+            # 14 fp64 VALU instructions (4 cycles per wave on a SIMD) and 4 DPP moves (2
+            # cycles) per level-row of a 128-column strip; a launch runs K levels over every
+            # row of ceil(W / output columns) strips (segment overlap and the edge strips'
+            # slower body not counted). frac: those cycles / the launch's cycles on every
+            # SIMD at the 2.4 GHz peak clock
+            oc = 128 - 4 * ((spl + 1) // 2)
+            level_rows = h * spl * -(-W // oc)
+            cyc = level_rows * (14 * 4 + 4 * 2) / (256 * 4)
+            line["roofline"]["valu"] = {
+                "bound": "valu", "cycles_per_simd_per_launch": round(cyc),
+                "peak_clock_mhz": 2400,
+                "frac": round(cyc / (kern_avg_ms * 1e-3 * 2.4e9), 4)}
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
                 if na == 1 else cpu_baseline_program(wl["rows"], W, na, C5_FLOWS,
