@@ -1096,24 +1096,6 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
             tail = nsteps % per;
         }
     }
-    // every K-step kernel instance the run launches: one empty launch each, so the first
-    // pass of the run does not bind its code object. (The ~0.3 ms a 20-step run loses after
-    // a 5-step warmup against a 20-step one is not this, nor the graph: eager launches
-    // lose it too -- profiles/r02c/gap/.)
-    if (passk_ok(e)) {
-        bool seen[mm::kMaxSteps + 1] = {};
-        for (long long s = 0, k = 0; s < nsteps; s += k) {
-            k = next_pass_len(e, nsteps - s);
-            if (seen[k]) continue;
-            seen[k] = true;
-            for (int red = 0; red <= (reduce_every > 0 ? 1 : 0); ++red) {
-                MM_HIP(mm::touch_passk((int)k, e->na, red != 0, true, e->s_comp, e->variant));
-                if (e->split)
-                    MM_HIP(mm::touch_passk((int)k, e->na, red != 0, false, e->s_comm, e->variant));
-            }
-        }
-        MM_HIP(hipDeviceSynchronize());
-    }
     // the eagerly launched passes: plan them now, which loads their kernels' code objects
     if (passk_ok(e) && tail > 0) {
         for (long long s = 0, k = 0; s < tail; s += k) {

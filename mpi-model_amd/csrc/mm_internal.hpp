@@ -52,10 +52,6 @@ hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, in
 // blocks (a.th = 4). a.nstrips = ceil(W / passk_out_cols(k)). red: every level's sums into
 // partials[wave][k][na]. variant bit 0: non-temporal stores.
 hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t s, int variant);
-// One-block launch of the K-step kernel instance launch_passk would use, with no waves to
-// run (every wave returns at its first test): binds the instance's code object ahead of
-// a timed run without touching any buffer. seg: segment schedule, else the border blocks.
-hipError_t touch_passk(int k, int na, bool red, bool seg, hipStream_t s, int variant);
 int passk_out_cols(int k);
 int passk_max_steps(int na);
 // largest segment (rows) whose buffer offsets stay below 2^31 at this pitch

@@ -1,7 +1,5 @@
 // mm_kernels_k.hip -- dispatch of the K-step kernel (templates: mm_passk.hpp, instances:
 // mm_passk_k1..10.hip) and the fixed-order level-sum finalize kernel.
-#include <cstring>
-
 #include "mm_passk.hpp"
 
 namespace mm {
@@ -72,28 +70,6 @@ int passk_waves_per_cu(int k, int na, bool red, int nt) {
         case 9: return passk_waves_k9(na, red, nt);
         case 10: return passk_waves_k10(na, red, nt);
         default: return 0;
-    }
-}
-
-hipError_t touch_passk(int k, int na, bool red, bool seg, hipStream_t s, int variant) {
-    PassArgs a;
-    memset(&a, 0, sizeof a);
-    a.seg = seg ? 1 : 0;
-    a.th = seg ? 16 : kBorderRows;
-    a.nstrips = 1;
-    a.waves_total = 0;  // the kernel's first test returns every wave
-    switch (k) {
-        case 1: return passk_launch_k1(na, red, a, s, variant);
-        case 2: return passk_launch_k2(na, red, a, s, variant);
-        case 3: return passk_launch_k3(na, red, a, s, variant);
-        case 4: return passk_launch_k4(na, red, a, s, variant);
-        case 5: return passk_launch_k5(na, red, a, s, variant);
-        case 6: return passk_launch_k6(na, red, a, s, variant);
-        case 7: return passk_launch_k7(na, red, a, s, variant);
-        case 8: return passk_launch_k8(na, red, a, s, variant);
-        case 9: return passk_launch_k9(na, red, a, s, variant);
-        case 10: return passk_launch_k10(na, red, a, s, variant);
-        default: return hipErrorInvalidValue;
     }
 }
 

@@ -705,7 +705,6 @@ template <int K, int MODE, int U, int NT, int NA, bool CHAIN>
 hipError_t launch_k3(bool red, const PassArgs& a, hipStream_t s) {
     long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
     if (a.xcd_remap) blocks = (blocks + 7) / 8 * 8;
-    if (blocks < 1) blocks = 1;  // touch_passk: one block whose waves all return at once
     const dim3 g((unsigned)blocks), b(kBlock);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
