@@ -46,7 +46,7 @@ struct PassArgs {
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
 hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);
-// K fused steps of a one-pass flow program (NA = 1: K 1..4, one diffusion; NA 2..4:
+// K fused steps of a one-pass flow program (NA = 1: K 1..10, one diffusion; NA 2..4:
 // K 1..2, diffusions and transfer chains) on overlapped strips (mm_passk_kernel,
 // mm_kernels_k.hip). a.seg: segment schedule, a.th / a.th_edge rows per wave; else 4-row
 // blocks (a.th = 4). a.nstrips = ceil(W / passk_out_cols(k)). red: every level's sums into

@@ -72,27 +72,28 @@ __device__ __forceinline__ void emit_one(double r, double u, int cnt, double& s,
 // Chain entries are read with compile-time indices only, so they are scalar loads of
 // the kernel arguments that the compiler hoists out of the row loop (a runtime index
 // into the by-value PassArgs turns into per-row global loads and vmcnt(0) waits that
-// drain the row prefetch).
+// drain the row prefetch). The attribute values sit in one 8-element register vector for
+// the chain, indexed by the wave-uniform a / b with s_set_gpr_idx (mm_passk.hpp chain_k);
+// a pad slot takes the outflows that leave the system.
 template <int NA>
 __device__ __forceinline__ void apply_chain(double (&u)[NA], int n, const signed char* ta,
                                             const signed char* tb, const double* tr) {
+    static_assert(NA < 8, "one pad slot");
+    typedef double dv8 __attribute__((ext_vector_type(8)));
+    dv8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = k < NA ? u[k] : 0.0;
 #pragma unroll
     for (int t = 0; t < kMaxChain; ++t) {
         if (t >= n) break;  // wave-uniform
-        const int a = ta[t], b = tb[t];
-        const double r = tr[t];
-        double src = 0.0;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) src = u[k];
-        const double out = r * src;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) u[k] = u[k] - out;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == b) u[k] = u[k] + out;
+        const int a = ta[t];
+        const int b = tb[t] >= 0 ? tb[t] : 7;
+        const double out = tr[t] * v[a];
+        v[a] = v[a] - out;
+        v[b] = v[b] + out;
     }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) u[k] = v[k];
 }
 
 // Raw values of one row as this lane sees them: its two columns + its edge column.

@@ -207,28 +207,30 @@ struct Lane {
 };
 
 // Transfers of a chain, in declared order, on one cell's attribute values: out = r*u_a;
-// u_a -= out; u_b += out (b < 0: the outflow leaves the system). Chain entries are read
-// with compile-time indices only (scalar loads of the kernel arguments).
+// u_a -= out; u_b += out (b < 0: the outflow leaves the system). a and b are wave-uniform
+// kernel arguments. The values sit in one 8-element register vector for the chain -- at
+// that width LLVM indexes it with s_set_gpr_idx (two v_mov per access) instead of a
+// select over every attribute per operand (36 v_cndmask per transfer and column) -- and a
+// pad slot takes the outflows that leave the system.
+typedef double dv8 __attribute__((ext_vector_type(8)));
 template <int NA>
 __device__ __forceinline__ void chain_k(double (&u)[NA], int n, const signed char* ta,
                                         const signed char* tb, const double* tr) {
+    static_assert(NA < 8, "one pad slot");
+    dv8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = k < NA ? u[k] : 0.0;
 #pragma unroll
     for (int t = 0; t < kMaxChain; ++t) {
         if (t >= n) break;  // wave-uniform
-        const int a = ta[t], b = tb[t];
-        const double r = tr[t];
-        double src = 0.0;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) src = u[k];
-        const double out = r * src;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == a) u[k] = u[k] - out;
-#pragma unroll
-        for (int k = 0; k < NA; ++k)
-            if (k == b) u[k] = u[k] + out;
+        const int a = ta[t];
+        const int b = tb[t] >= 0 ? tb[t] : 7;
+        const double out = tr[t] * v[a];
+        v[a] = v[a] - out;
+        v[b] = v[b] + out;
     }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) u[k] = v[k];
 }
 
 // Pre-chain, then per diffusing attribute out = rate*u, s = out/cnt, d = u - out for this
