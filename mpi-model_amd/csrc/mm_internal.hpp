@@ -7,7 +7,9 @@
 namespace mm {
 
 constexpr int kMaxAttr = 4;     // SoA attributes per fused pass (config C5: 4)
-constexpr int kMaxChain = 8;    // elementwise transfers before / after a pass's diffusion
+constexpr int kMaxChain = 4;    // elementwise transfers before / after a pass's diffusion
+                                // (a longer chain starts a new pass; 4 holds config C5's
+                                // chain and, against 8, frees kernel-argument SGPRs: C5 -8 %)
 constexpr int kStripCols = 128; // columns per wave: 64 lanes x double2 (16 B per lane)
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;

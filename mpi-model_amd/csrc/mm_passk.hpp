@@ -213,6 +213,9 @@ struct Lane {
 // select over every attribute per operand (36 v_cndmask per transfer and column) -- and a
 // pad slot takes the outflows that leave the system.
 typedef double dv8 __attribute__((ext_vector_type(8)));
+#ifndef MM_CHAIN_CAP
+#define MM_CHAIN_CAP kMaxChain  // transfers a chain may hold (tuning: fewer unrolled slots)
+#endif
 template <int NA>
 __device__ __forceinline__ void chain_k(double (&u)[NA], int n, const signed char* ta,
                                         const signed char* tb, const double* tr) {
@@ -221,7 +224,7 @@ __device__ __forceinline__ void chain_k(double (&u)[NA], int n, const signed cha
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = k < NA ? u[k] : 0.0;
 #pragma unroll
-    for (int t = 0; t < kMaxChain; ++t) {
+    for (int t = 0; t < MM_CHAIN_CAP; ++t) {
         if (t >= n) break;  // wave-uniform
         const int a = ta[t];
         const int b = tb[t] >= 0 ? tb[t] : 7;

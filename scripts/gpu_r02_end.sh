@@ -19,3 +19,5 @@ PSTEPS=20 PMCSTEPS=20 OUT=$O/prof_c3_k10 WL=c3 bash scripts/gpu_profile.sh > $O/
 grep -h '"kernel_name"\|"avg_us"\|hbm_bytes_per_launch' $O/prof_c3_k10/summary.json
 OUT=$O/prof_c3_k8 WL=c3 bash scripts/gpu_profile.sh > $O/prof_c3_k8.log 2>&1 || { echo "profile k8 failed"; tail -30 $O/prof_c3_k8.log; exit 3; }
 grep -h '"kernel_name"\|"avg_us"\|hbm_bytes_per_launch' $O/prof_c3_k8/summary.json
+OUT=$O/prof_c5 WL=c5 bash scripts/gpu_profile.sh > $O/prof_c5.log 2>&1 || { echo "profile c5 failed"; tail -30 $O/prof_c5.log; exit 3; }
+grep -h '"kernel_name"\|"avg_us"\|hbm_bytes_per_launch' $O/prof_c5/summary.json
