@@ -540,7 +540,12 @@ double pass_cost(int k) {
 int next_pass_len(const mm_engine* e, long long n) {
     const int kp = passk_steps(e);
     long long best_p = (n + kp - 1) / kp;
-    const bool big = (double)e->d.h * (double)e->d.W >= 268435456.0;
+    // the planner's slabs: >= 2^28 cells in >= 256 strips. With fewer strips the two edge
+    // strips (the general body, which spills at K >= 9) weigh more and deep passes lose:
+    // 16384^2, 20 steps: 10 + 10 2.85 ms vs 7 + 7 + 6 2.61 ms; 32768 columns at 8192 and
+    // 32768 rows: 10 + 10 wins by 7 % (profiles/r02_end/k10tune, profiles/r02c).
+    const bool big = (double)e->d.h * (double)e->d.W >= 268435456.0 &&
+                     nstrips_k(e, mm::kMaxSteps) >= 256;
     if (e->plan && e->kpass == 0 && e->na == 1 && big && n > kp) {
         long long kx = mm::passk_max_steps(1);
         if (e->d.nranks > 1) kx = std::min<long long>(kx, e->min_rows);

@@ -75,9 +75,10 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
 
 
 def test_pass_planner_plans(gpu, monkeypatch):
-    """mm_pass_plan on a 16384^2 slab: short runs take fewer, deeper passes (20 steps:
-    10 + 10), long runs stay at K = 8; MM_PASS_PLAN=0 / a fixed K give balanced passes."""
-    with gpu.Engine(16384, 16384) as e:
+    """mm_pass_plan on an 8192 x 32768 slab: short runs take fewer, deeper passes (20
+    steps: 10 + 10), long runs stay at K = 8; MM_PASS_PLAN=0 and slabs with fewer strips
+    (16384^2) or cells (4096^2) give balanced passes of K."""
+    with gpu.Engine(8192, 32768) as e:
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [10, 10]
         assert e.pass_plan(16) == [8, 8]
@@ -85,20 +86,24 @@ def test_pass_planner_plans(gpu, monkeypatch):
         assert e.pass_plan(1000) == [8] * 125
         assert e.pass_plan(0) == []
     monkeypatch.setenv("MM_PASS_PLAN", "0")
-    with gpu.Engine(16384, 16384) as e:
+    with gpu.Engine(8192, 32768) as e:
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [7, 7, 6]
     monkeypatch.delenv("MM_PASS_PLAN")
+    with gpu.Engine(16384, 16384) as e:  # 152 strips: no planner
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [7, 7, 6]
     with gpu.Engine(4096, 4096) as e:  # small slab: K = 7, no planner
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [7, 7, 6]
 
 
 def test_driver_length_run_two_deep_passes(gpu, O):
-    """The driver's 20-step run on a 16384^2 grid: two K = 10 passes (the planner),
-    equal to 20 single steps bit for bit on three bands widened by the 20-row cone (top
-    edge, middle, bottom edge: every column, so both edge strips), total conserved."""
-    H = W = 16384
+    """A 20-step run on an 8192 x 32768 slab (the rows one GPU of a 4-GPU c3 run holds):
+    two K = 10 passes (the planner), equal to 20 single steps bit for bit on three bands
+    widened by the 20-row cone (top edge, middle, bottom edge: every column, so both edge
+    strips), total conserved."""
+    H, W = 8192, 32768
     steps = 20
     with gpu.Engine(H, W) as e:
         e.fill_random(0)
