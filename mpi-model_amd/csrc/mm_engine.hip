@@ -506,7 +506,9 @@ int passk_steps(const mm_engine* e) {
     // step of the round-2 sweeps (profiles/r02/sweep_k_*.log, profiles/r02c/sweep_*x32768:
     // 32768^2, 16384^2 and the 8192- and 4096-row slabs of 32768 columns favour 8, 4096^2
     // with its short segments 7; K <= 4 leaves the VALU idle behind the HBM stream)
-    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->d.h * (double)e->d.W >= 134217728.0 ? 8 : 7);
+    // (sized by the chain's thinnest slab, the same on every rank: every rank of a halo
+    // chain must run the same passes, or the K-row exchanges would not pair up)
+    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->min_rows * (double)e->d.W >= 134217728.0 ? 8 : 7);
     int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
     if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
     return std::max(1, k);
@@ -544,7 +546,7 @@ int next_pass_len(const mm_engine* e, long long n) {
     // strips (the general body, which spills at K >= 9) weigh more and deep passes lose:
     // 16384^2, 20 steps: 10 + 10 2.85 ms vs 7 + 7 + 6 2.61 ms; 32768 columns at 8192 and
     // 32768 rows: 10 + 10 wins by 7 % (profiles/r02_end/k10tune, profiles/r02c).
-    const bool big = (double)e->d.h * (double)e->d.W >= 268435456.0 &&
+    const bool big = (double)e->min_rows * (double)e->d.W >= 268435456.0 &&  // rank-invariant
                      nstrips_k(e, mm::kMaxSteps) >= 256;
     if (e->plan && e->kpass == 0 && e->na == 1 && big && n > kp) {
         long long kx = mm::passk_max_steps(1);
