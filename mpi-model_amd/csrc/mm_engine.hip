@@ -389,11 +389,13 @@ long long seg_wave_count(long long n, long long ns, long long r, long long re) {
 
 // Edge-strip segment length / interior segment length of a k-step pass. The two edge
 // strips run the general body, several times slower per row than the branch-free one,
-// and at K >= 9 it spills; their segments are cut shorter so they end with the rest
-// (profiles/r02b/k9k10/edge_*: K = 10 at 0.5 takes 1.5x the pass time of 0.1).
+// and at K >= 8 it spills; their segments are cut shorter so they end with the rest
+// (profiles/r02b/k9k10/edge_*: K = 10 at 0.5 takes 1.5x the pass time of 0.1;
+// profiles/r02_end/edge/sweep_*: K = 8 at 0.3 is 3 % faster than 0.5 at 16384^2, within
+// 0.2 % at 32768^2).
 double seg_edge_of(const mm_engine* e, int k) {
     if (e->seg_edge > 0.0) return e->seg_edge;
-    return k >= 10 ? 0.1 : (k == 9 ? 0.2 : 0.5);
+    return k >= 10 ? 0.1 : (k == 9 ? 0.2 : (k == 8 ? 0.3 : 0.5));
 }
 
 // Segment plan of rows [lo, hi) of a k-step pass: r rows per interior-strip segment, re
