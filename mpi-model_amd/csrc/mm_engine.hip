@@ -391,11 +391,14 @@ long long seg_wave_count(long long n, long long ns, long long r, long long re) {
 // strips run the general body, several times slower per row than the branch-free one,
 // and at K >= 8 it spills; their segments are cut shorter so they end with the rest
 // (profiles/r02b/k9k10/edge_*: K = 10 at 0.5 takes 1.5x the pass time of 0.1;
-// profiles/r02_end/edge/sweep_*: K = 8 at 0.3 is 3 % faster than 0.5 at 16384^2, within
-// 0.2 % at 32768^2).
+// profiles/r02_end/edge/sweep_*: on slabs of >= 2^26 cells K = 6..8 at 0.3 are 1-3 %
+// faster than at 0.5 at 16384^2 and within 0.2 % at 32768^2; the short segments of
+// smaller slabs keep 0.5).
 double seg_edge_of(const mm_engine* e, int k) {
     if (e->seg_edge > 0.0) return e->seg_edge;
-    return k >= 10 ? 0.1 : (k == 9 ? 0.2 : (k == 8 ? 0.3 : 0.5));
+    if (k >= 10) return 0.1;
+    if (k == 9) return 0.2;
+    return (double)e->d.h * (double)e->d.W >= 67108864.0 ? 0.3 : 0.5;
 }
 
 // Segment plan of rows [lo, hi) of a k-step pass: r rows per interior-strip segment, re
