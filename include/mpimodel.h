@@ -187,7 +187,10 @@ int mm_fill(mm_engine* eng, int attr, int mode, double value, unsigned long long
 int mm_upload(mm_engine* eng, int attr, const double* host);
 int mm_download(mm_engine* eng, int attr, double* host);
 
-/* Flow program. src/Model.hpp:23-27 stores one Flow; the engine keeps an ordered list. */
+/* Flow program. src/Model.hpp:23-27 stores one Flow; the engine keeps an ordered list.
+ * One step applies the flows in order; the engine groups them into kernel passes (a
+ * diffusion per attribute with up to 4 same-cell transfers before and after it; longer
+ * chains start a new pass), which changes no result. */
 int mm_clear_flows(mm_engine* eng);
 int mm_add_flow(mm_engine* eng, int kind, int a, int b, double rate);
 
