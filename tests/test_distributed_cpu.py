@@ -4,7 +4,7 @@ without GPUs.
 Each rank owns the slab mm_partition_rows gives it, keeps `depth` ghost rows above and
 below, and before every `depth` steps sends its first `depth` rows to rank-1 and its
 last `depth` rows to rank+1 -- the exchange the engine does with ncclSend/ncclRecv
-(mm_engine.hip halo_rccl; depth K for the K-step kernel, K <= 8). Steps are computed
+(mm_engine.hip halo_rccl; depth K for the K-step kernel, K <= 10). Steps are computed
 with the oracle on the slab; the gathered grid must equal the single-process oracle
 bit for bit (src/Model.hpp's row slabs, generalised to every cell and every step).
 """
@@ -98,6 +98,8 @@ def worker(rank, world, port, H, W, rate, steps, depth, out_q):
     # passes, and slabs exactly as thin as the depth (the engine caps K by min slab rows)
     (2, 40, 29, 9, 3), (3, 41, 33, 10, 4), (4, 16, 21, 9, 4), (2, 16, 19, 17, 8),
     (3, 13, 17, 7, 4),
+    # the planner's deepest passes (K = 10): two passes of 10 on slabs of 12 and 13 rows
+    (2, 25, 19, 20, 10),
 ])
 def test_row_slabs_with_halo_exchange_bit_exact(O, world, H, W, steps, depth):
     ctx = tmp.get_context("spawn")
