@@ -19,7 +19,7 @@ import mpimodel as mm  # noqa: E402
 
 ENV_KEYS = ("MM_FUSE", "MM_PASSK", "MM_STEPS_PER_PASS", "MM_ROWS_PER_WAVE",
             "MM_ROWS_PER_WAVE2", "MM_KERNEL_VARIANT", "MM_XCD_REMAP", "MM_SEG_WAVES",
-            "MM_SEG_EDGE")
+            "MM_SEG_EDGE", "MM_BORDER_SEG", "MM_SELF_HALO", "MM_PASS_PLAN")
 
 PRESETS = {
     # segment-scheduled K-step kernel: K x waves per slot x edge-strip length x
