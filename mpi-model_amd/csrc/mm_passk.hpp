@@ -85,6 +85,9 @@ constexpr int kSeg = 0;                  // MODE value of the segment schedule
 #ifndef MM_LEVEL_BARRIER
 #define MM_LEVEL_BARRIER 0  // scheduling barrier after every this many levels (0: none)
 #endif
+#ifndef MM_ROW_BARRIER
+#define MM_ROW_BARRIER 1  // steady loop: scheduling barrier after every this many rows (0: none)
+#endif
 #ifndef MM_SEG_U1
 #define MM_SEG_U1 8  // rows prefetched per wave, one attribute
 #endif
@@ -497,7 +500,9 @@ __device__ __forceinline__ void seg_steady(const PassArgs& A, const Lane& c, con
                 if ((K - j) % MM_LEVEL_BARRIER == MM_LEVEL_BARRIER - 1) __builtin_amdgcn_sched_barrier(0);
 #endif
             }
-            __builtin_amdgcn_sched_barrier(0);
+#if MM_ROW_BARRIER
+            if (t % MM_ROW_BARRIER == MM_ROW_BARRIER - 1 || t == U - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
         }
     }
 }
