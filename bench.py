@@ -268,8 +268,8 @@ def main():
     if rank == 0:
         kern_avg_ms = kern_ms / max(n_launch, 1)
         launches_per_step = n_launch / max(timing_steps, 1)
-        spl = max(plan) if info["kernel"] == 2 else 1  # steps of the dominant (longest) pass
-        kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel"}[info["kernel"]]
+        spl = max(plan) if info["kernel"] in (2, 3) else 1  # steps of the dominant (longest) pass
+        kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel", 3: "mm_wide_kernel"}[info["kernel"]]
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         traffic = None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -321,16 +321,20 @@ def main():
             },
             "check": {"total_rel_drift": cons},
         }
-        if info["kernel"] == 2 and na == 1 and kern_ms > 0:
-            # the K-step kernel's other roof: its steady-state loop issues
-            # 14 fp64 VALU instructions (4 cycles per wave on a SIMD) and 4 DPP moves (2
-            # cycles) per level-row of a 128-column strip; a launch runs K levels over every
-            # row of ceil(W / output columns) strips (segment overlap and the edge strips'
-            # slower body not counted). frac: those cycles / the launch's cycles on every
-            # SIMD at the 2.4 GHz peak clock
-            oc = 128 - 4 * ((spl + 1) // 2)
+        if info["kernel"] in (2, 3) and na == 1 and kern_ms > 0 and len(set(plan)) == 1:
+            # the K-step kernels' other roof: the steady-state loop issues,
+            # per level-row of a strip, 7 fp64 VALU instructions per column of a lane (4
+            # cycles per wave on a SIMD) and 4 DPP moves (2 cycles) -- mm_passk_kernel: 2
+            # columns per lane, 128-column strips, 4*ceil(K/2) halo columns; mm_wide_kernel:
+            # 4 columns per lane, 256-column strips, 8*ceil(K/4) halo columns. A launch runs
+            # K levels over every row of ceil(W / output columns) strips (segment overlap,
+            # LDS hand-offs and the edge strips' slower body not counted). frac: those
+            # cycles / the launch's cycles on every SIMD at the 2.4 GHz peak clock. Only
+            # when every pass of the run has the same K (the timed average is one kernel's)
+            cols = 2 if info["kernel"] == 2 else 4
+            oc = 64 * cols - 2 * cols * (-(-spl // cols))
             level_rows = h * spl * -(-W // oc)
-            cyc = level_rows * (14 * 4 + 4 * 2) / (256 * 4)
+            cyc = level_rows * (7 * cols * 4 + 4 * 2) / (256 * 4)
             line["roofline"]["valu"] = {
                 "bound": "valu", "cycles_per_simd_per_launch": round(cyc),
                 "peak_clock_mhz": 2400,

@@ -86,9 +86,12 @@ typedef struct mm_info {
     long long waves_per_pass;  /* waves launched per pass */
     long long steps_done;      /* steps run since the last fill/upload */
     int fused_attrs;           /* attributes carried per fused pass */
-    int steps_per_launch;      /* steps fused per kernel pass (temporal blocking), 1..4 */
+    int steps_per_launch;      /* steps fused per kernel pass (temporal blocking): 1..10
+                                  (mm_passk_kernel), 4/8/12/16/20 (mm_wide_kernel) */
     int kernel;                /* step kernel: 0 mm_pass_kernel (one step per pass),
-                                  2 mm_passk_kernel (steps_per_launch steps per pass) */
+                                  2 mm_passk_kernel (steps_per_launch steps per pass, all
+                                  levels in one wave), 3 mm_wide_kernel (steps_per_launch
+                                  steps per pass, the levels split over 4 waves) */
     int halo_depth;            /* ghost rows one border exchange fills (= steps per pass) */
     int graph_state;           /* 0 no graph used yet, 1 steps replayed as hipGraphs,
                                   -1 stream capture refused: steps run eagerly (graph_note) */
@@ -165,13 +168,16 @@ int mm_device_synchronize(int device);
 /* ---- engine ------------------------------------------------------------- */
 /* Replaces the per-worker CellularSpace construction (src/Model.hpp:149) and the
  * init loop (src/Model.hpp:154-157): device buffers are (h + 2*kGhost) x pitch fp64 per
- * attribute (kGhost = 10 ghost rows above and below, the deepest K-step pass), two of
+ * attribute (kGhost = 20 ghost rows above and below, the deepest K-step pass), two of
  * them (Jacobi ping-pong).
  * With nranks > 1 the steps per kernel pass (and so the halo depth) are capped by the
  * thinnest slab of the chain: RCCL engines all-reduce it at creation; host-transport
- * engines assume mm_partition_rows slabs (floor(H/nranks) rows at least).
+ * engines accept mm_partition_rows slabs only (floor(H/nranks) rows at least) and
+ * return MM_ERR_INVALID otherwise.
  * Environment: MM_PASSK=0 (or MM_FUSE=0) runs one step per kernel pass, MM_GRAPH=0
- * disables the hipGraph replay, MM_STEPS_PER_PASS (1..10; fixes K), MM_PASS_PLAN=0
+ * disables the hipGraph replay, MM_WIDE=0/1 selects the level-split K-step kernel for
+ * one-diffusion programs, MM_STEPS_PER_PASS (1..10, or 4/8/12/16/20 with the wide
+ * kernel; fixes K), MM_PASS_PLAN=0
  * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
  * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal policy)
  * override tuning; MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
@@ -238,7 +244,7 @@ int mm_clear_history(mm_engine* eng);
 /* MM_HALO_HOST transport: copy this slab's first/last nrows owned rows of every
  * attribute out (top/bottom: n_attr*nrows*W doubles each, [attr][row][col]), and the
  * neighbours' rows into the nrows ghost rows above / below (NULL = no neighbour on
- * that side). nrows is info.halo_depth (1..4). Replaces the scalar halo messages
+ * that side). nrows is info.halo_depth (1..kGhost = 20). Replaces the scalar halo messages
  * src/Model.hpp:202-204 <-> :228-230 with whole rows. mm_halo_export/import move one
  * row (nrows = 1). */
 int mm_halo_export_rows(mm_engine* eng, int nrows, double* top, double* bottom);
@@ -247,14 +253,14 @@ int mm_halo_export(mm_engine* eng, double* top, double* bottom);
 int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
 
 /* Test/debug: copy nrows rows starting at local row row0 (owned rows are 0..h-1, ghost
- * rows -4..-1 and h..h+3) of the current buffer of one attribute to host (W each). */
+ * rows -kGhost..-1 and h..h+kGhost-1, kGhost = 20) of the current buffer of one attribute to host (W each). */
 int mm_debug_read_rows(mm_engine* eng, int attr, long long row0, long long nrows, double* host);
 
 /* Measurement: with timing on, mm_run records a HIP event pair around every
  * step-kernel launch on the stream it is launched on; mm_timing returns the
  * number of timed launches, their summed duration (ms) and the average algorithmic
  * bytes one launch moves: 16 B per cell of its rows per attribute (read once, written
- * once), for a one-step launch and a fused two-step launch alike. */
+ * once), whether the launch advances one step or K. */
 int mm_set_timing(mm_engine* eng, int on);
 int mm_timing(mm_engine* eng, long long* n_launches, double* total_ms, double* bytes_per_launch);
 

@@ -33,7 +33,6 @@
 #ifndef MM_DRIVER_HPP
 #define MM_DRIVER_HPP
 
-#include <cassert>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -41,6 +40,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -152,31 +152,60 @@ inline void merge_files(const std::vector<std::string>& names) {
     }
 }
 
-// The control messages of worker k (1-based): what the reference's master sends.
+// The control messages of worker k (1-based): what the reference's master sends, and the
+// numbers they carry (computed here on every rank, so nothing depends on the bytes).
 struct Descriptors {
     char partition[MM_WIRE_LEN];
     char flow[MM_WIRE_LEN];
     int owner;
+    int x0, y0, h, w;
+    bool fits;  // both messages fit the reference's 23 bytes (with the NUL)
 };
+
+// A descriptor past the reference's 23-char buffer (e.g. "10|10000:10000|0.100000", or a
+// large rate through %lf) cannot go on the reference's wire. It is a limit of the wire
+// format, not of the run: the message goes out as 23 NUL bytes, every rank uses the numbers
+// it computed itself, and rank 0 says so once on stderr.
+inline void wire_limit_warning(bool fits, int rank) {
+    static bool said = false;
+    if (fits || said || rank != 0) return;
+    said = true;
+    std::cerr << "mpimodel: a control descriptor does not fit the reference's " << MM_WIRE_LEN
+              << "-byte message (src/Model.hpp:71,81); sending NUL bytes, every rank uses its "
+                 "own partition and owner" << std::endl;
+}
 
 inline Descriptors make_descriptors(const Layout& L, const FlowSpec& f, int H, int W, int P,
                                     int k) {
     Descriptors d;
-    int x0, y0, h, w;
     if (L.rect)
-        check(mm_partition_rect_reference(H, W, L.lines, L.columns, k, &x0, &y0, &h, &w));
+        check(mm_partition_rect_reference(H, W, L.lines, L.columns, k, &d.x0, &d.y0, &d.h, &d.w));
     else
-        check(mm_partition_reference(H, W, P, k, &x0, &y0, &h, &w));
-    check(mm_wire_format_partition(d.partition, MM_WIRE_LEN, x0, y0, h, w));
+        check(mm_partition_reference(H, W, P, k, &d.x0, &d.y0, &d.h, &d.w));
+    // mm_wire_format_* leave an all-NUL buffer when the text does not fit
+    d.fits = mm_wire_format_partition(d.partition, MM_WIRE_LEN, d.x0, d.y0, d.h, d.w) == MM_OK;
     if (f.whole_grid) {  // extension: every cell is a source; no owner, no source cell
         d.owner = 0;
-        check(mm_wire_format_flow(d.flow, MM_WIRE_LEN, 0, -1, -1, f.rate));
+        d.fits = mm_wire_format_flow(d.flow, MM_WIRE_LEN, 0, -1, -1, f.rate) == MM_OK && d.fits;
     } else {
         d.owner = L.rect ? mm_owner_rect_reference(L.space_height, (int)f.src_x, (int)f.src_y)
                          : mm_owner_reference(H, P, (int)f.src_x);
-        check(mm_wire_format_flow(d.flow, MM_WIRE_LEN, d.owner, (int)f.src_x, (int)f.src_y, f.rate));
+        d.fits = mm_wire_format_flow(d.flow, MM_WIRE_LEN, d.owner, (int)f.src_x, (int)f.src_y,
+                                     f.rate) == MM_OK && d.fits;
     }
     return d;
+}
+
+// The reference's conservation check (src/Model.hpp:95), two-sided and size-aware, as a
+// check that survives NDEBUG: a violation throws std::runtime_error like the reference's
+// MPI failures (src/MPIImpl.cpp:7-8).
+inline void check_conservation(double sum, double initial) {
+    if (!(std::fabs(sum - initial) <= 1e-9 * initial)) {
+        char msg[160];
+        std::snprintf(msg, sizeof msg, "mpimodel: conservation violated: sum %.17g, initial %.17g",
+                      sum, initial);
+        throw std::runtime_error(msg);
+    }
 }
 
 // The worker body: one slab on one GPU. Returns the slab sum (src/Model.hpp:237-240).
@@ -273,8 +302,10 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         rep.blocks.clear();
         for (int k = 1; k <= P; ++k) {
             const Descriptors dk = make_descriptors(L, f, (int)H, (int)W, P, k);
-            int x0, y0, h, w;
-            check(mm_wire_parse_partition(dk.partition, MM_WIRE_LEN, &x0, &y0, &h, &w));
+            wire_limit_warning(dk.fits, rank);
+            int x0 = dk.x0, y0 = dk.y0, h = dk.h, w = dk.w;
+            if (dk.fits)  // what a worker reads back (src/Model.hpp:139-146)
+                check(mm_wire_parse_partition(dk.partition, MM_WIRE_LEN, &x0, &y0, &h, &w));
             rep.blocks.insert(rep.blocks.end(), {x0, y0, h, w});
             if (!single) MPI_Send(dk.partition, MM_WIRE_LEN, MPI_CHAR, k, MM_TAG_PARTITION, comm);
         }
@@ -295,10 +326,12 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         char part[MM_WIRE_LEN + 1] = {0}, flow[MM_WIRE_LEN + 1] = {0};
         MPI_Recv(part, MM_WIRE_LEN, MPI_CHAR, 0, MM_TAG_PARTITION, comm, MPI_STATUS_IGNORE);
         MPI_Recv(flow, MM_WIRE_LEN, MPI_CHAR, 0, MM_TAG_FLOW, comm, MPI_STATUS_IGNORE);
-        int x0, y0, h, w, fx, fy, rate_atoi;
+        int x0, y0, h, w, fx, fy, rate_atoi, parsed_owner;
         double rate;
-        check(mm_wire_parse_partition(part, MM_WIRE_LEN, &x0, &y0, &h, &w));
-        check(mm_wire_parse_flow(flow, MM_WIRE_LEN, &owner, &fx, &fy, &rate_atoi, &rate));
+        // a descriptor past the wire's 23 bytes arrives as NUL bytes: keep the local numbers
+        if (mm_wire_parse_partition(part, MM_WIRE_LEN, &x0, &y0, &h, &w) == MM_OK &&
+            mm_wire_parse_flow(flow, MM_WIRE_LEN, &parsed_owner, &fx, &fy, &rate_atoi, &rate) == MM_OK)
+            owner = parsed_owner;
         if (L.rect) std::cout << flow << std::endl;  // src/ModelRectangular.hpp:158
     }
 
@@ -321,7 +354,7 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         rep.steps = n;
         rep.gcups = seconds > 0 ? (double)H * W * n / seconds / 1e9 : 0.0;
         rep.final_sum = local;
-        assert(std::fabs(local - rep.initial_sum) <= 1e-9 * rep.initial_sum);
+        check_conservation(local, rep.initial_sum);
         if (files) merge_files(std::vector<std::string>(1, file));
     } else if (rank == 0) {
         // src/Model.hpp:88-95: per-worker sums, received in rank order
@@ -346,7 +379,7 @@ void run_model(const MPI_Comm& comm, const FlowSpec& f, double time, double time
         rep.gcups = rep.seconds > 0 ? (double)H * W * n / rep.seconds / 1e9 : 0.0;
         // the reference's check, made two-sided and size-aware (src/Model.hpp:95)
         rep.final_sum = acc;
-        assert(std::fabs(acc - rep.initial_sum) <= 1e-9 * rep.initial_sum);
+        check_conservation(acc, rep.initial_sum);
         if (files) {
             // src/Model.hpp:110-111: file names in rank order, tag = rank
             std::vector<std::string> names;

@@ -100,7 +100,10 @@ struct mm_engine {
 
     int th = 8;              // rows per wave, one-step kernel
     bool passk = true;       // mm_passk_kernel for one-pass programs (MM_PASSK=0: one step per pass)
-    int kpass = 0;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps; 0: auto)
+    int wide = -1;           // mm_wide_kernel for one-diffusion programs where K allows
+                             // (MM_WIDE=0/1; -1 auto: slabs of >= kWideCells cells)
+    int kpass = 0;           // steps per pass, one attribute (MM_STEPS_PER_PASS, 1..kMaxSteps,
+                             // with MM_WIDE also the wide kernel's K; 0: auto)
     int kpass_multi = 2;     // steps per pass, several attributes (MM_STEPS_PER_PASS, 1..2)
     bool plan = true;        // pass-length planner (MM_PASS_PLAN=0: balanced passes of K)
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
@@ -108,6 +111,7 @@ struct mm_engine {
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
+    int bpc[2][2][mm::kMaxWide + 1] = {};                       // wide kernel blocks/CU cache
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -234,7 +238,8 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
-// Launch a one-step pass (kpass == 0) or a K-step pass (mm_passk_kernel) covering `rows`
+// Launch a one-step pass (kpass == 0), a K-step pass (kpass = K > 0: mm_passk_kernel;
+// kpass = -K: mm_wide_kernel) covering `rows`
 // rows on the compute stream, with an event pair around it when timing. Algorithmic
 // bytes: every cell of those rows read once and written once per attribute.
 int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, bool time_it,
@@ -250,6 +255,8 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
     }
     if (kpass > 0)
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
+    else if (kpass < 0)
+        MM_HIP(mm::launch_wide(-kpass, red, A, e->s_comp, e->variant));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -442,11 +449,122 @@ void seg_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lon
     A.waves_a = A.waves_total = seg_wave_count(n, ns, r, A.th_edge);
 }
 
+bool passk_ok(const mm_engine* e);
+
+// The level-split kernel runs this pass: one attribute, one diffusion, K one of its
+// instances, MM_WIDE on.
+constexpr double kWideCells = 268435456.0;  // 2^28: 16384^2, 8192 x 32768 and up
+
+bool wide_on(const mm_engine* e) {
+    // auto: sized by the chain's thinnest slab (rank-invariant, like every plan input)
+    return e->wide > 0 || (e->wide < 0 && (double)e->min_rows * (double)e->d.W >= kWideCells);
+}
+
+bool use_wide(const mm_engine* e, int k) {
+    return wide_on(e) && e->na == 1 && passk_ok(e) && mm::wide_has(k);
+}
+
+long long nstrips_wide(const mm_engine* e, int k) {
+    const int oc = mm::wide_out_cols(k);
+    return (e->d.W + oc - 1) / oc;
+}
+
+// Segment plan of rows [lo, hi) for the wide kernel: one workgroup per strip segment, r
+// rows per interior-strip segment and re per edge-strip segment, the smallest r for which
+// the blocks fit seg_waves x the chip's resident blocks. Auto: 4 per resident slot, halved
+// (down to 1) while segments are shorter than 24 K rows -- a segment pays 3K - 1 pipeline
+// iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
+// profiles/r03/kernel_table).
+void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
+    const int nt = e->variant & 1;
+    int& bpc = e->bpc[red ? 1 : 0][nt][k];
+    if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, red, nt));
+    const long long n = hi - lo, ns = A.nstrips;
+    const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
+    const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
+    const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
+    auto re_of = [&](long long rr) {
+        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
+    };
+    auto plan = [&](double sw) {
+        const long long want = std::max<long long>(1, (long long)(sw * e->ncu * bpc));
+        long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
+        r = std::min(std::max<long long>(r, 16), maxr);
+        while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
+        return std::min(r, maxr);
+    };
+    long long r;
+    if (e->seg_waves > 0.0) {
+        r = plan(e->seg_waves);
+    } else {
+        double sw = 4.0;
+        r = plan(sw);
+        while (sw > 1.0 && r < 24LL * k) {
+            sw *= 0.5;
+            r = plan(sw);
+        }
+    }
+    A.seg = 1;
+    A.th = (int)r;
+    A.th_edge = (int)re_of(r);
+    A.ra0 = (int)lo;
+    A.ra1 = (int)hi;
+    A.rb0 = A.rb1 = 0;
+    A.waves_a = A.waves_total = seg_wave_count(n, ns, r, A.th_edge);
+}
+
+// A k-step pass on the level-split kernel: enqueue_passk's two-stream structure; the border
+// rows are one `depth`-row segment per strip and side (ranges a and b of one launch).
+int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
+    const long long h = e->d.h;
+    const int depth = k;
+    const bool red = mask != 0;
+    mm::PassArgs A;
+    fill_args(e, e->passes[0], A);
+    A.nstrips = (int)nstrips_wide(e, k);
+    A.xcd_remap = e->xcd;
+    long long total_blocks = 0;
+    if (e->split && h >= 2 * depth + 1) {
+        MM_TRY(split_begin(e, depth));
+        wide_range(e, k, red, A, depth, h - depth);
+        const long long interior = A.waves_total;
+        mm::PassArgs B = A;
+        B.xcd_remap = 0;
+        B.th = B.th_edge = depth;
+        B.ra0 = 0;
+        B.ra1 = depth;
+        B.rb0 = (int)(h - depth);
+        B.rb1 = (int)h;
+        B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
+        B.waves_total = 2 * B.waves_a;
+        B.partial_base = interior;
+        MM_HIP(mm::launch_wide(k, red, B, e->s_comm, 0));
+        MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
+        e->comm_live = true;
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
+        total_blocks = interior + B.waves_total;
+        if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+    } else {
+        if (e->split) MM_TRY(unsplit_halo(e, depth));
+        wide_range(e, k, red, A, 0, h);
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, red, A, h, time_it, -k));
+        total_blocks = A.waves_total;
+    }
+    if (red)
+        MM_HIP(mm::launch_finalize_levels(e->partials, total_blocks, k, e->na, mask, e->hist,
+                                          e->hist_n, e->hist_cap, e->s_comp));
+    e->cur ^= 1;
+    return MM_OK;
+}
+
 // k fused steps of the one-pass program in one mm_passk_kernel pass; bit j of `mask`:
 // append the sums after step j+1 of the pass to the history. Same two-stream structure as
 // enqueue_pass, with a k-row halo (every k steps): the interior rows run as segments
 // beside the exchange, the border rows as 4-row blocks after it.
 int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
+    if (use_wide(e, k)) return enqueue_wide(e, k, mask, time_it);
     const long long h = e->d.h;
     const int depth = k;
     const bool red = mask != 0;
@@ -504,6 +622,8 @@ bool passk_ok(const mm_engine* e) {
     return true;
 }
 
+constexpr int kWideAuto = 16;  // auto steps per pass of the wide kernel
+
 // Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
 // past the thinnest slab of the chain (every rank sends K owned rows each way).
 int passk_steps(const mm_engine* e) {
@@ -513,7 +633,12 @@ int passk_steps(const mm_engine* e) {
     // with its short segments 7; K <= 4 leaves the VALU idle behind the HBM stream)
     // (sized by the chain's thinnest slab, the same on every rank: every rank of a halo
     // chain must run the same passes, or the K-row exchanges would not pair up)
-    const int k1 = e->kpass > 0 ? e->kpass : ((double)e->min_rows * (double)e->d.W >= 134217728.0 ? 8 : 7);
+    // wide (mm_wide_kernel): auto K = kWideAuto
+    const int kauto = (wide_on(e) && e->na == 1)
+                          ? kWideAuto
+                          : ((double)e->min_rows * (double)e->d.W >= 134217728.0 ? 8 : 7);
+    int k1 = e->kpass > 0 ? e->kpass : kauto;
+    if (!(wide_on(e) && e->na == 1)) k1 = std::min(k1, mm::kMaxSteps);  // mm_passk_kernel's K
     int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
     if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
     return std::max(1, k);
@@ -544,8 +669,64 @@ double pass_cost(int k) {
 // fewer, longer passes (up to kMaxSteps, capped by the chain's thinnest slab) and takes
 // the plan of least modelled time: 20 steps run as 10 + 10, a long run stays at K = 8
 // (1000 steps: 125 passes).
+// A pass of k steps has a kernel: the wide one (use_wide) or mm_passk_kernel (k <= 10).
+bool pass_len_ok(const mm_engine* e, long long k) {
+    return k >= 1 && (k <= mm::kMaxSteps || use_wide(e, (int)k));
+}
+
+// Modelled time of one k-step pass on a large slab with the wide kernel on (HIP-event pass
+// times at 32768^2, profiles/r03/kernel_table: mm_passk_kernel K <= 7 stream-bound at
+// ~3.5 ms, K = 8 / 9 / 10 at 3.66 / 4.14 / 4.62 ms; mm_wide_kernel K = 4 / 8 / 12 / 16 / 20
+// at 3.69 / 3.68 / 4.90 / 6.22 / 8.13 ms), in ms.
+double wide_plan_cost(const mm_engine* e, int k) {
+    if (use_wide(e, k)) {
+        switch (k) {
+            case 4: return 3.69;
+            case 8: return 3.68;
+            case 12: return 4.90;
+            case 16: return 6.22;
+            default: return 8.13;
+        }
+    }
+    if (k <= 7) return 3.50;
+    return k == 8 ? 3.66 : (k == 9 ? 4.14 : 4.62);
+}
+
+// Steps of the first pass of the cheapest plan of n steps (wide on, K auto): a dynamic
+// program over the pass lengths both kernels have (capped by the chain's thinnest slab).
+// Runs longer than kDpMax steps start with a pass of the best per-step length (K = 16).
+int wide_plan_first(const mm_engine* e, long long n, int kcap) {
+    constexpr int kDpMax = 256;
+    if (n > kDpMax) return std::min(kWideAuto, kcap);
+    std::vector<double> best((size_t)n + 1, 1e300);
+    std::vector<int> first((size_t)n + 1, 1);
+    best[0] = 0.0;
+    for (long long m = 1; m <= n; ++m)
+        for (int k = 1; k <= std::min<long long>(m, kcap); ++k) {
+            if (!pass_len_ok(e, k)) continue;
+            const double c = wide_plan_cost(e, k) + best[(size_t)(m - k)];
+            if (c < best[(size_t)m] * (1.0 - 1e-9)) {
+                best[(size_t)m] = c;
+                first[(size_t)m] = k;
+            }
+        }
+    return first[(size_t)n];
+}
+
 int next_pass_len(const mm_engine* e, long long n) {
     const int kp = passk_steps(e);
+    if (wide_on(e) && e->na == 1) {
+        if (e->kpass == 0 && e->plan) {
+            int cap = mm::kMaxWide;
+            if (e->d.nranks > 1) cap = (int)std::min<long long>(cap, e->min_rows);
+            return wide_plan_first(e, n, cap);
+        }
+        // configured K: passes of K while n >= K, a shorter run in one pass when a kernel
+        // has that length, else the longest length a kernel has
+        long long k = std::min<long long>(n, kp);
+        while (k > 1 && !pass_len_ok(e, k)) --k;
+        return (int)std::max<long long>(1, k);
+    }
     long long best_p = (n + kp - 1) / kp;
     // the planner's slabs: >= 2^28 cells in >= 256 strips. With fewer strips the two edge
     // strips (the general body, which spills at K >= 9) weigh more and deep passes lose:
@@ -605,6 +786,26 @@ long long gcd_ll(long long a, long long b) {
     return a;
 }
 
+// Every rank of an RCCL chain must run the same passes, or the K-row exchanges would not
+// pair up: a graph replays the passes of its length, the eager fallback plans the rest of
+// the run. So whether a capture worked is agreed over the chain (one all-reduce of a flag,
+// at the first capture of each graph: every rank captures the same keys at the same call).
+int agree_capture(mm_engine* e, bool ok) {
+    if (!e->comm || e->d.nranks <= 1) return ok ? MM_OK : MM_ERR_HIP;
+    int v = ok ? 1 : 0;
+    int* dv = reinterpret_cast<int*>(e->sum_tmp);
+    if (hipMemcpy(dv, &v, sizeof v, hipMemcpyHostToDevice) != hipSuccess ||
+        ncclAllReduce(dv, dv, 1, ncclInt32, ncclMin, e->comm, e->s_comm) != ncclSuccess ||
+        hipStreamSynchronize(e->s_comm) != hipSuccess ||
+        hipMemcpy(&v, dv, sizeof v, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MM_ERR_RCCL, "capture agreement all-reduce failed");
+    if (v) return MM_OK;
+    return ok ? fail(MM_ERR_HIP, "another rank's stream capture was refused") : MM_ERR_HIP;
+}
+
+int capture_graph(mm_engine* e, long long len, long long reduce_every, long long phase,
+                  hipGraphExec_t* out, int* flip);
+
 int get_graph(mm_engine* e, long long len, long long reduce_every, long long phase,
               hipGraphExec_t* out, int* flip) {
     auto key = std::make_tuple(e->cur, len, reduce_every, phase);
@@ -614,6 +815,16 @@ int get_graph(mm_engine* e, long long len, long long reduce_every, long long pha
         *flip = it->second.second;
         return MM_OK;
     }
+    const int rc = capture_graph(e, len, reduce_every, phase, out, flip);
+    const std::string why = g_last_error;
+    const int ra = agree_capture(e, rc == MM_OK);
+    if (rc != MM_OK) g_last_error = why;
+    return rc != MM_OK ? rc : ra;
+}
+
+int capture_graph(mm_engine* e, long long len, long long reduce_every, long long phase,
+                  hipGraphExec_t* out, int* flip) {
+    auto key = std::make_tuple(e->cur, len, reduce_every, phase);
     const int cur0 = e->cur;
     MM_HIP(hipStreamBeginCapture(e->s_comp, hipStreamCaptureModeThreadLocal));
     const int rc = enqueue_steps(e, phase + 1, len, reduce_every, false);
@@ -659,7 +870,7 @@ int ensure_partials(mm_engine* e) {
     const long long ns = nstrips_k(e, mm::kMaxSteps);
     const long long border = 2 * ((mm::kGhost + mm::kBorderRows - 1) / mm::kBorderRows) + 2;
     need = std::max(need, (ns * ((e->d.h + 7) / 8 + border) + 16) *
-                              std::max(mm::kMaxSteps, 2 * mm::kMaxAttr));
+                              std::max(mm::kMaxWide, 2 * mm::kMaxAttr));
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
@@ -803,9 +1014,10 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->th = choose_th(e);
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
+    if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
-        if (v >= 1 && v <= mm::kMaxSteps) e->kpass = v;
+        if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && mm::wide_has(v)))) e->kpass = v;
         if (v >= 1) e->kpass_multi = std::min(v, 2);
     }
     if (const char* p = std::getenv("MM_PASS_PLAN")) e->plan = std::atoi(p) != 0;
@@ -893,6 +1105,14 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         e->min_rows = hmin;
         e->split = true;
     } else if (d.nranks > 1 && d.halo_mode == MM_HALO_HOST) {
+        // the host transport sizes K and the halo depth from the standard partition
+        // (min_rows above), so a neighbour of a caller-chosen thinner slab could be asked
+        // for rows it does not own: only mm_partition_rows slabs are accepted
+        long long x0 = 0, hh = 0;
+        if (mm_partition_rows(d.H, d.nranks, d.rank, &x0, &hh) != MM_OK || x0 != d.x_init ||
+            hh != d.h)
+            return cleanup(fail(MM_ERR_INVALID, "mm_engine_create: MM_HALO_HOST slabs must be "
+                                                "mm_partition_rows(H, nranks, rank)"));
         e->split = true;
     }
     // default program: one Exponencial flow on attribute 0 is set by the caller
@@ -931,7 +1151,16 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->bytes_device = (long long)e->bytes;
     info->n_passes = (int)e->passes.size();
     const int spl = steps_per_launch(e);
-    if (passk_ok(e)) {  // the whole-slab segment plan of one pass
+    if (passk_ok(e) && use_wide(e, spl)) {  // one workgroup of 4 waves per strip segment
+        mm::PassArgs A;
+        std::memset(&A, 0, sizeof A);
+        A.nstrips = (int)nstrips_wide(e, spl);
+        wide_range(e, spl, false, A, 0, e->d.h);
+        info->rows_per_wave = A.th;
+        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl);
+        info->kernel = 3;
+        info->seg_waves_per_cu = e->bpc[0][e->variant & 1][spl] * mm::wide_waves_per_block(spl);
+    } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);
         A.nstrips = (int)nstrips_k(e, spl);
@@ -1092,6 +1321,11 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
     if (nsteps == 0) return MM_OK;
     MM_TRY(set_device(e));
     const long long phase = reduce_every > 0 ? e->steps_done % reduce_every : 0;
+    // the history the run appends, grown now: growing it inside mm_run would drop (and
+    // re-capture) the graph prepared here
+    const long long entries =
+        reduce_every > 0 ? (phase + nsteps) / reduce_every - phase / reduce_every : 0;
+    MM_TRY(reserve_history(e, entries));
     const long long per = e->timing ? 0 : graph_per(e, nsteps, reduce_every);
     long long tail = nsteps;
     if (per > 0) {
@@ -1114,8 +1348,13 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
             k = next_pass_len(e, tail - s);
             mm::PassArgs A;
             std::memset(&A, 0, sizeof A);
-            A.nstrips = (int)nstrips_k(e, (int)k);
-            seg_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
+            if (use_wide(e, (int)k)) {
+                A.nstrips = (int)nstrips_wide(e, (int)k);
+                wide_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
+            } else {
+                A.nstrips = (int)nstrips_k(e, (int)k);
+                seg_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
+            }
         }
     }
     return MM_OK;

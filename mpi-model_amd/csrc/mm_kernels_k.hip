@@ -1,6 +1,7 @@
-// mm_kernels_k.hip -- dispatch of the K-step kernel (templates: mm_passk.hpp, instances:
-// mm_passk_k1..10.hip) and the fixed-order level-sum finalize kernel.
-#include "mm_passk.hpp"
+// mm_kernels_k.hip -- dispatch of the K-step kernels (templates: mm_passk.hpp and
+// mm_wide.hpp, instances: mm_passk_k1..10.hip, mm_wide_k*.hip) and the fixed-order
+// level-sum finalize kernel.
+#include "mm_wide.hpp"
 
 namespace mm {
 
@@ -86,6 +87,37 @@ hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t 
         case 8: return passk_launch_k8(na, red, a, s, variant);
         case 9: return passk_launch_k9(na, red, a, s, variant);
         case 10: return passk_launch_k10(na, red, a, s, variant);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool wide_has(int k) { return k == 4 || k == 8 || k == 12 || k == 16 || k == 20; }
+
+int wide_out_cols(int k) {
+    return kWideStrip - 2 * kWideCols * ((k + kWideCols - 1) / kWideCols);
+}
+
+int wide_waves_per_block(int k) { return wide_has(k) ? 4 : 0; }
+
+int wide_blocks_per_cu(int k, bool red, int nt) {
+    switch (k) {
+        case 4: return wide_blocks_k4(red, nt);
+        case 8: return wide_blocks_k8(red, nt);
+        case 12: return wide_blocks_k12(red, nt);
+        case 16: return wide_blocks_k16(red, nt);
+        case 20: return wide_blocks_k20(red, nt);
+        default: return 0;
+    }
+}
+
+hipError_t launch_wide(int k, bool red, const PassArgs& a, hipStream_t s, int variant) {
+    if (a.waves_total <= 0) return hipSuccess;
+    switch (k) {
+        case 4: return wide_launch_k4(red, a, s, variant);
+        case 8: return wide_launch_k8(red, a, s, variant);
+        case 12: return wide_launch_k12(red, a, s, variant);
+        case 16: return wide_launch_k16(red, a, s, variant);
+        case 20: return wide_launch_k20(red, a, s, variant);
         default: return hipErrorInvalidValue;
     }
 }

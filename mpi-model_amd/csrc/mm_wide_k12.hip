@@ -1,0 +1,13 @@
+// mm_wide_k12.hip -- instances of the level-split K-step kernel (mm_wide.hpp) for K = 12:
+// 3 level(s) per wave, 4 waves per workgroup.
+#include "mm_wide.hpp"
+
+namespace mm {
+
+hipError_t wide_launch_k12(bool red, const PassArgs& a, hipStream_t s, int v) {
+    return wide_launch2<3, 4>(red, a, s, v);
+}
+
+int wide_blocks_k12(bool red, int nt) { return wide_blocks<3, 4>(red, nt); }
+
+}  // namespace mm

@@ -183,3 +183,34 @@ def test_whole_grid_flow_program(tmp_path, O, np_):
         lines.extend(files[k].decode().splitlines())
     want = [f"{x}\t{y}\t{v[x, y]:g}" for x in range(H) for y in range(W)]
     assert lines == want
+
+
+@pytest.mark.parametrize("H,W,sx,sy,fits", [
+    (1000, 1000, 999, 500, True),       # "10|999:500|0.100000": fits the 23-byte message
+    (20000, 10001, 19999, 10000, False),  # "10|19999:10000|0.100000": one byte too long
+])
+def test_point_flow_many_workers_wire_limit(tmp_path, H, W, sx, sy, fits):
+    # 10 workers and 5-digit coordinates: the flow descriptor no longer fits the
+    # reference's 23-char message (src/Model.hpp:81,85). That is a limit of the wire format,
+    # not of the run: the message goes out as NUL bytes, every rank uses its own owner and
+    # partition, rank 0 warns once, and the flow is applied and conserved as usual
+    import json
+    stdout_err = []
+    run = tmp_path / "run"
+    out = tmp_path / "output"
+    run.mkdir()
+    out.mkdir()
+    env = dict(os.environ)
+    env["MM_WRITE_OUTPUT"] = "0"
+    p = subprocess.run([MPIRUN, "-np", "11", os.path.join(REPO, "examples", "point_flow_main"),
+                        str(H), str(W), str(sx), str(sy), "2.2", "0.1"], cwd=run,
+                       capture_output=True, text=True, timeout=240, env=env)
+    stdout_err.append(p.stdout + p.stderr)
+    assert p.returncode == 0, stdout_err[0][-3000:]
+    rep = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rep["owner"] == sx // (H // 10) + 1 == 10  # src/Model.hpp:80
+    assert float.fromhex(rep["final_sum"]) == pytest.approx(H * W, rel=1e-12)
+    assert len(rep["blocks"]) == 10
+    assert rep["blocks"][9] == [9 * (H // 10), 0, H // 10, W]
+    warned = "does not fit the reference's 23-byte message" in p.stderr
+    assert warned == (not fits)

@@ -66,10 +66,17 @@ CHAINS = [(64, 300, 2), (37, 130, 3), (27, 257, 3), (100, 488, 3), (41, 200, 8),
           (24, 257, 8), (16, 130, 8), (9, 124, 8), (300, 700, 2)]
 
 
-@pytest.mark.parametrize("k", [10, 9, 8, 7, 6, 5, 4, 3, 2, 1])
+WIDE_K = (4, 8, 12, 16, 20)  # mm_wide_kernel instances
+
+
+@pytest.mark.parametrize("k,wide", [(k, 0) for k in (10, 9, 8, 7, 6, 5, 4, 3, 2, 1)]
+                         + [(k, 1) for k in WIDE_K])
 @pytest.mark.parametrize("H,W,G", CHAINS)
-def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k):
-    engines = make_chain(gpu, monkeypatch, H, W, G, env={"MM_STEPS_PER_PASS": k})
+def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k, wide):
+    # wide = 1: the level-split kernel wherever the depth is one of its K (a thinner
+    # slab caps the depth to min h, which may leave mm_passk_kernel to run it)
+    env = {"MM_STEPS_PER_PASS": k, "MM_WIDE": wide}
+    engines = make_chain(gpu, monkeypatch, H, W, G, env=env)
     try:
         for e in engines:
             e.fill_random(0)
@@ -77,7 +84,7 @@ def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k):
         info = engines[0].info()
         min_h = H // G
         assert info["halo_depth"] == min(k, min_h) == info["steps_per_launch"]
-        assert info["kernel"] == 2
+        assert info["kernel"] == (3 if wide and info["halo_depth"] in WIDE_K else 2)
         steps = 2 * info["halo_depth"] + 1  # two full passes and a shorter one
         run_chain(engines, steps)
         got = gather(engines)
@@ -86,13 +93,16 @@ def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k):
     assert np.array_equal(got, O.field_step(O.fill_random(H, W), 0.3, steps=steps))
 
 
+@pytest.mark.parametrize("env", [{}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8},
+                                 {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12}],
+                         ids=lambda e: ",".join(f"{k[3:]}={v}" for k, v in e.items()) or "default")
 @pytest.mark.parametrize("reduce_every", [1, 3])
 @pytest.mark.parametrize("H,W,G", [(100, 488, 3), (41, 200, 8), (300, 700, 2), (130, 257, 4)])
-def test_deep_halo_chain_step_sums(gpu, O, monkeypatch, H, W, G, reduce_every):
+def test_deep_halo_chain_step_sums(gpu, O, monkeypatch, H, W, G, reduce_every, env):
     # per-step sums of every slab (partials at partial_base offsets: interior segments
     # first, then the border blocks) summed over the slabs in rank order
-    steps = 9
-    engines = make_chain(gpu, monkeypatch, H, W, G)
+    steps = 9 if not env else 2 * env["MM_STEPS_PER_PASS"] + 1
+    engines = make_chain(gpu, monkeypatch, H, W, G, env=env)
     try:
         for e in engines:
             e.fill_random(0)
@@ -178,7 +188,7 @@ def test_host_halo_rejects_more_steps_than_depth(gpu, monkeypatch):
         with pytest.raises(gpu.MMError):
             e.run(d + 1)
         with pytest.raises(gpu.MMError):
-            e.halo_export(11)  # more rows than the ghost zone (kGhost = 10) holds
+            e.halo_export(21)  # more rows than the ghost zone (kGhost = 20) holds
     finally:
         close(engines)
 

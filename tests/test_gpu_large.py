@@ -1,5 +1,7 @@
 """Full-size configs on the GPU (BASELINE.json configs[2..3]): C3 = 32768^2 and
-C4 = 16384^2 fp64, 8 steps (two K=4 passes) of the production path.
+C4 = 16384^2 fp64 on the production path: 8 steps, and the driver's exact 20-step run
+(bench.py --steps 20: the default planner's passes, one K = 20 pass of the level-split
+kernel; with MM_WIDE=0 round 2's 10 + 10 passes of mm_passk_kernel).
 
 The whole grid is far too big for the oracle, so parity is pinned by
   * three 64-row bands -- the top edge, the rows around an interior segment boundary of
@@ -46,7 +48,7 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
         s0 = e.sums()[0]
         e.add_diffuse(0, RATE)
         info = e.info()
-        assert info["steps_per_launch"] >= 4 and info["kernel"] == 2
+        assert info["steps_per_launch"] >= 4 and info["kernel"] in (2, 3)
         e.run(STEPS)
         e.synchronize()
         s1 = e.sums()[0]
@@ -74,50 +76,95 @@ def test_full_size_bands_conservation_symmetry(gpu, O, N):
 
 
 
+WIDE_K = (4, 8, 12, 16, 20)
+
+
 def test_pass_planner_plans(gpu, monkeypatch):
-    """mm_pass_plan on an 8192 x 32768 slab: short runs take fewer, deeper passes (20
-    steps: 10 + 10), long runs stay at K = 8; MM_PASS_PLAN=0 and slabs with fewer strips
-    (16384^2) or cells (4096^2) give balanced passes of K."""
-    with gpu.Engine(8192, 32768) as e:
-        e.add_diffuse(0, RATE)
-        assert e.pass_plan(20) == [10, 10]
-        assert e.pass_plan(16) == [8, 8]
-        assert e.pass_plan(9) == [9]
-        assert e.pass_plan(1000) == [8] * 125
-        assert e.pass_plan(0) == []
+    """mm_pass_plan. Slabs of >= 2^28 cells run the level-split kernel: the planner's
+    cheapest plan over both kernels' lengths -- one K = 20 pass for the driver's 20 steps,
+    K = 16 passes for long runs. MM_PASS_PLAN=0: passes of K = 16 and a tail.
+    MM_WIDE=0 (round 2): 10 + 10 on 8192 x 32768, K = 8 for long runs. Smaller slabs
+    (4096^2) keep mm_passk_kernel's balanced passes of K = 7."""
+    for H, W in ((8192, 32768), (16384, 16384)):
+        with gpu.Engine(H, W) as e:
+            e.add_diffuse(0, RATE)
+            assert e.info()["kernel"] == 3
+            assert e.pass_plan(20) == [20]
+            assert e.pass_plan(16) == [16]
+            assert e.pass_plan(12) == [12]
+            assert e.pass_plan(9) == [9]
+            assert e.pass_plan(0) == []
+            p = e.pass_plan(1000)
+            assert sum(p) == 1000 and len(p) <= 63
+            assert all(k in WIDE_K or k <= 10 for k in p)
+            assert p.count(16) >= 55
     monkeypatch.setenv("MM_PASS_PLAN", "0")
     with gpu.Engine(8192, 32768) as e:
         e.add_diffuse(0, RATE)
-        assert e.pass_plan(20) == [7, 7, 6]
+        assert e.pass_plan(20) == [16, 4]
     monkeypatch.delenv("MM_PASS_PLAN")
+    monkeypatch.setenv("MM_WIDE", "0")
+    with gpu.Engine(8192, 32768) as e:
+        e.add_diffuse(0, RATE)
+        assert e.info()["kernel"] == 2
+        assert e.pass_plan(20) == [10, 10]
+        assert e.pass_plan(1000) == [8] * 125
     with gpu.Engine(16384, 16384) as e:  # 152 strips: no planner
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [7, 7, 6]
-    with gpu.Engine(4096, 4096) as e:  # small slab: K = 7, no planner
+    monkeypatch.delenv("MM_WIDE")
+    with gpu.Engine(4096, 4096) as e:  # small slab: mm_passk_kernel, K = 7, no planner
         e.add_diffuse(0, RATE)
+        assert e.info()["kernel"] == 2
         assert e.pass_plan(20) == [7, 7, 6]
 
 
-def test_driver_length_run_two_deep_passes(gpu, O):
-    """A 20-step run on an 8192 x 32768 slab (the rows one GPU of a 4-GPU c3 run holds):
-    two K = 10 passes (the planner), equal to 20 single steps bit for bit on three bands
-    widened by the 20-row cone (top edge, middle, bottom edge: every column, so both edge
-    strips), total conserved."""
-    H, W = 8192, 32768
-    steps = 20
+def driver_run_bands(gpu, O, monkeypatch, H, W, wide, plan):
+    """`steps` = sum(plan) steps under the default planner (or MM_WIDE=0): the planned
+    passes, each one launch; three bands -- top edge, an interior segment boundary of the
+    pass's plan, bottom edge: every column, so both edge strips -- against 20 single steps
+    of the oracle on the band widened by the dependency cone; total conserved."""
+    steps = sum(plan)
+    if not wide:
+        monkeypatch.setenv("MM_WIDE", "0")
+    # the segment plan of the run's first pass (info describes the configured K's plan)
+    monkeypatch.setenv("MM_STEPS_PER_PASS", str(plan[0]))
+    with gpu.Engine(H, W) as probe:
+        probe.add_diffuse(0, RATE)
+        seg_info = probe.info()
+    monkeypatch.delenv("MM_STEPS_PER_PASS")
     with gpu.Engine(H, W) as e:
+        if not wide:
+            monkeypatch.delenv("MM_WIDE")
         e.fill_random(0)
         s0 = e.sums()[0]
         e.add_diffuse(0, RATE)
+        assert e.pass_plan(steps) == plan
+        info = e.info()
+        assert info["kernel"] == (3 if wide else 2)
         e.set_timing(True)
         e.run(steps)
         n_launch, _, _ = e.timing()
         e.set_timing(False)
-        assert n_launch == 2
+        assert n_launch == len(plan)
         s1 = e.sums()[0]
-        bands = {b: e.read_rows(b, 64) for b in (0, H // 2 - 32, H - 64)}
+        bands = {b: e.read_rows(b, 64) for b in sorted(set(bands_for(H, seg_info)))}
     assert abs(s1 - s0) <= 1e-12 * s0
     for b, got in bands.items():
         lo, hi = max(0, b - steps), min(H, b + 64 + steps)
         want = band_oracle(O, H, W, lo, hi, steps, RATE)[b - lo:b - lo + 64]
         assert np.array_equal(got, want), (b, int(np.count_nonzero(got != want)))
+
+
+@pytest.mark.parametrize("wide,plan", [(1, [20]), (0, [10, 10])], ids=["wide", "passk"])
+def test_driver_length_run_slab(gpu, O, monkeypatch, wide, plan):
+    """The 8192 x 32768 slab one GPU of a 4-GPU c3 run holds, 20 steps."""
+    driver_run_bands(gpu, O, monkeypatch, 8192, 32768, wide, plan)
+
+
+@pytest.mark.parametrize("wide,plan", [(1, [20]), (0, [10, 10])], ids=["wide", "passk"])
+def test_driver_config_full_grid(gpu, O, monkeypatch, wide, plan):
+    """The exact configuration the driver times (bench.py --steps 20, c3): the whole
+    32768^2 grid, 20 steps under the default planner -- one K = 20 pass of the level-split
+    kernel -- and under MM_WIDE=0 the 10 + 10 passes round 2's driver line timed."""
+    driver_run_bands(gpu, O, monkeypatch, 32768, 32768, wide, plan)

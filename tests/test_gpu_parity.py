@@ -190,31 +190,44 @@ FUSE_ENVS = [{"MM_PASSK": 0}, {}] + [
     {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 5, 6, 7, 8, 9, 10)
 ] + [{"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0},
      {"MM_XCD_REMAP": 1}, {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16}]
+# the level-split kernel (mm_wide_kernel) at each of its K, and its plan / order knobs
+WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)] + [
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_SEG_WAVES": 64},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}]
 
 
 def env_id(env):
     return ",".join(f"{k[3:]}={v}" for k, v in env.items()) or "default"
 
 
-@pytest.mark.parametrize("env", FUSE_ENVS, ids=env_id)
-@pytest.mark.parametrize("shape", [(1, 1), (2, 3), (3, 5), (5, 2), (37, 53), (130, 257),
-                                   (257, 300), (64, 1000), (9, 124), (70, 125), (33, 241),
-                                   (100, 488)])
+FUSE_SHAPES = [(1, 1), (2, 3), (3, 5), (5, 2), (37, 53), (130, 257), (257, 300), (64, 1000),
+               (9, 124), (70, 125), (33, 241), (100, 488)]
+
+
+@pytest.mark.parametrize("env", FUSE_ENVS + WIDE_ENVS, ids=env_id)
+@pytest.mark.parametrize("shape", FUSE_SHAPES + [(45, 700), (257, 512), (70, 1025), (300, 233)])
 def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
     # K steps per pass (temporal blocking) against the oracle's single steps; step counts
-    # that are not multiples of K end with a shorter pass
+    # that are not multiples of K end with a shorter pass. Run lengths: 1, 3, 5 (the
+    # passes of mm_passk_kernel), then K and K + 3 (a whole pass of the configured K, then
+    # one with a tail)
     H, W = shape
+    k = int(env.get("MM_STEPS_PER_PASS", 20 if env.get("MM_WIDE") else 10))
+    runs = (1, 3, 5, k, k + 3)
     v0 = O.fill_random(H, W)
     want = {}
     ref = v0
-    for k in range(1, 10):
+    for s in range(1, sum(runs) + 1):
         ref = O.field_step(ref, 0.3)
-        want[k] = ref
+        want[s] = ref
     e = make_env_engine(gpu, monkeypatch, H, W, **env)
     e.fill_random(0)
     e.add_diffuse(0, 0.3)
     done = 0
-    for steps in (1, 3, 5):  # 1, 4, 9 steps in total
+    for steps in runs:
         e.run(steps)
         done += steps
         assert np.array_equal(e.download(), want[done]), (env, shape, done)
@@ -224,10 +237,13 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
 @pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 3}, {"MM_STEPS_PER_PASS": 2},
                                  {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
                                  {"MM_STEPS_PER_PASS": 7},
-                                 {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}], ids=env_id)
+                                 {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}]
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
+                         ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
-    H, W, steps = 130, 257, 12
+    H, W = 130, 257
+    steps = max(12, 2 * int(env.get("MM_STEPS_PER_PASS", 0)) + 3)
     v = O.fill_random(H, W)
     e = make_env_engine(gpu, monkeypatch, H, W, **env)
     e.upload(v)
@@ -248,13 +264,14 @@ def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
         assert abs(a - b) <= 1e-12 * b
 
 
-@pytest.mark.parametrize("k", [2, 3, 4, 6, 7, 8, 9, 10])
-def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k):
+@pytest.mark.parametrize("k,wide", [(k, 0) for k in (2, 3, 4, 6, 7, 8, 9, 10)]
+                         + [(k, 1) for k in (4, 8, 12, 16, 20)])
+def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k, wide):
     # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
-    # multiple of the graph length, so the tail runs eagerly (K = 10: a graph holds 60
-    # steps -- an even number of flips and whole reduction periods -- so run 130)
-    H, W, steps = 300, 700, (50 if k < 10 else 130)
-    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k)
+    # multiple of the graph length, so the tail runs eagerly (K >= 10: a graph holds
+    # 6K steps -- an even number of flips and whole reduction periods -- so run 13K)
+    H, W, steps = 300, 700, (50 if k < 10 else 13 * k)
+    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k, MM_WIDE=wide)
     e.fill_random(0)
     e.add_diffuse(0, 0.2)
     e.run(steps, 3)
@@ -366,9 +383,10 @@ def test_engine_rejects_bad_shapes(gpu):
             e.point_apply(8, 0, 1.0, 0.1)
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 4, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("k,wide", [(k, 0) for k in (1, 2, 3, 4, 6, 7, 8, 9, 10)]
+                         + [(k, 1) for k in (4, 8, 12, 16, 20)])
 @pytest.mark.parametrize("graph", [0, 1])
-def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
+def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph, wide):
     # The RCCL halo path on one GPU: one rank whose two neighbours are itself
     # (MM_SELF_HALO). Border rows go through ncclSend/ncclRecv on the comm stream, the
     # interior rows run meanwhile, the border rows after the event join -- eagerly and
@@ -379,7 +397,7 @@ def test_rccl_halo_path_single_rank(gpu, O, monkeypatch, k, graph):
     depth = k
     steps = 2 * depth  # two passes: afterwards the current buffer's ghost rows hold the
                        # rows exchanged in the first pass (the initial state's)
-    env = {"MM_SELF_HALO": 1, "MM_GRAPH": graph}
+    env = {"MM_SELF_HALO": 1, "MM_GRAPH": graph, "MM_WIDE": wide}
     env.update({"MM_PASSK": 0} if k == 1 else {"MM_STEPS_PER_PASS": k})
     for key, v in env.items():
         monkeypatch.setenv(key, str(v))
