@@ -19,6 +19,7 @@ timing  : W untimed warmup steps, then exactly K steps on the production path (h
 
 Launch: python bench.py [--gpus 1] [--steps 1000] [--warmup 50]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+        (--halo host: the host transport over gloo, N ranks on however many GPUs exist)
 """
 import argparse
 import json
@@ -73,6 +74,13 @@ def parse():
                          "price the exchange + interior/border split")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample length (oracle port, rank 0, N=1)")
+    ap.add_argument("--halo", default="rccl", choices=("rccl", "host"),
+                    help="N>1: RCCL K-row exchange (one GPU per rank), or the host transport "
+                         "over gloo between passes (any number of ranks on the GPUs present, "
+                         "e.g. N ranks sharing one GPU)")
+    ap.add_argument("--grid", type=int, nargs=2, metavar=("H", "W"),
+                    help="tests: override the workload's grid")
+    ap.add_argument("--dump", help="tests: save each rank's slab to DUMP.rank<r>.npy")
     return ap.parse_args()
 
 
@@ -164,6 +172,113 @@ def cpu_baseline_program(H, W, na, flows, seconds):
                       f"(scalar C, one core, no MPI found), {el:.1f} s"}
 
 
+def valu_roof(passes, h, W, kern_avg_ms):
+    """The K-step kernels' other roof: the steady-state loop issues, per
+    level-row of a strip, 7 fp64 VALU instructions per column of a lane (4 cycles per wave
+    on a SIMD) and 4 DPP moves (2 cycles). `passes`: (k, kernel, columns per lane, strips)
+    of every launch the timed average covers (mm_pass_kernel); a launch runs k levels over
+    every row of its strips (segment overlap, LDS hand-offs and the edge strips' slower body
+    not counted). frac: the launches' mean cycles per SIMD / the mean launch's cycles at the
+    2.4 GHz peak clock. None unless every launch is a K-step kernel."""
+    if not passes or kern_avg_ms <= 0 or any(kern not in (2, 3) for _, kern, _, _ in passes):
+        return None
+    cyc = sum(h * k * strips * (7 * cols * 4 + 4 * 2) / (256 * 4)
+              for k, _, cols, strips in passes) / len(passes)
+    return {"bound": "valu", "cycles_per_simd_per_launch": round(cyc), "peak_clock_mhz": 2400,
+            "frac": round(cyc / (kern_avg_ms * 1e-3 * 2.4e9), 4)}
+
+
+def make_line(*, workload, wl, N, ranks, H, W, h, na, steps, warmup, el, plan, info,
+              kern_ms, n_launch, timing_steps, bytes_per_launch, passes, traffic, cons, halo,
+              self_halo):
+    """The driver's JSON line (no I/O): value = whole-job GCUPS = all ranks' cell-updates /
+    the max-over-ranks wall time `el` of exactly `steps` steps."""
+    gcups = H * W * steps / el / 1e9
+    kern_avg_ms = kern_ms / max(n_launch, 1)
+    spl = max(plan) if info["kernel"] in (2, 3) and plan else 1  # steps of the longest pass
+    kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel", 3: "mm_wide_kernel"}[info["kernel"]]
+    achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
+    if info["graph_state"] == 1:
+        path = f"hipGraph replay ({info['graph_launches']} graph launches)"
+    elif info["graph_state"] == -1:
+        path = f"eager launches: graph capture refused ({info['graph_note']})"
+    else:
+        path = "eager launches (no graph)"
+    if N == 1:
+        par = "row-slab x1" + (" (self-halo: RCCL exchange with itself)" if self_halo else "")
+    elif halo == "host":
+        par = (f"row-slab x{N} ranks on {ranks['gpus']} GPU(s), host halo: K border rows "
+               f"over gloo between passes")
+    else:
+        par = f"row-slab x{N} + RCCL halo"
+    plan_s = '+'.join(map(str, plan)) if len(plan) <= 8 else f"{spl} (x{len(plan)})"
+    line = {
+        "metric": "cell-updates/s (GCUPS) per step + % of HBM roofline",
+        "value": round(gcups, 3),
+        "unit": "GCUPS",
+        "n_gpus": ranks["gpus"],
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(el * 1e3 / steps, 5),
+        "higher_is_better": True,
+        "scaling": wl["scaling"],
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
+                "seed 0x4D50494D, generated on the device",
+        "config": {"workload": f"{workload}: {wl['desc']}", "grid": [H, W],
+                   "path": f"{path}, {kname}, {len(plan)} pass(es) of {plan_s} fused steps",
+                   "ranks": N, "rows_per_gpu": h, "n_attr": na, "rate": RATE,
+                   "parallelism": par,
+                   "passes_per_step": info["n_passes"],
+                   "rows_per_wave": info["rows_per_wave"]},
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "kernel": kname,
+            "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "steps_per_launch": spl,
+            "launches_per_step": n_launch / max(timing_steps, 1),
+            # BASELINE.md's formula: GCUPS x 16 B x A / 8 TB/s (per GPU); above 1.0
+            # when K steps share one HBM round trip (temporal blocking)
+            "equivalent_frac": round(gcups / ranks["gpus"] * 16.0 * na / HBM_PEAK_GBS, 4),
+        },
+        "check": {"total_rel_drift": cons},
+    }
+    if na == 1:
+        v = valu_roof(passes, h, W, kern_avg_ms)
+        if v:
+            line["roofline"]["valu"] = v
+    return line
+
+
+def gloo_exchange(rank, N):
+    """Host transport of the K-row halo between passes (src/Model.hpp:202-204,224-235 made
+    whole-row and K deep): this slab's first rows go to rank-1, its last rows to rank+1, the
+    neighbours' rows come back for the ghost rows above / below."""
+    import torch
+    import torch.distributed as dist
+
+    def ex(top, bottom, k):
+        reqs, above, below = [], None, None
+        if rank > 0:
+            above = torch.empty(top.shape, dtype=torch.float64)
+            reqs += [dist.isend(torch.from_numpy(top), rank - 1), dist.irecv(above, rank - 1)]
+        if rank < N - 1:
+            below = torch.empty(bottom.shape, dtype=torch.float64)
+            reqs += [dist.isend(torch.from_numpy(bottom), rank + 1), dist.irecv(below, rank + 1)]
+        for r in reqs:
+            r.wait()
+        return (None if above is None else above.numpy(),
+                None if below is None else below.numpy())
+    return ex
+
+
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
@@ -174,20 +289,28 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N > 1 needs one process per GPU (torch.distributed.run)")
     N = world
+    host = N > 1 and args.halo == "host"
 
     import torch
     import torch.distributed as dist
     if N > 1:
-        dist.init_process_group("gloo")  # control plane only; data moves on RCCL
+        dist.init_process_group("gloo")  # control plane (and the host halo); data on RCCL
 
     if wl["scaling"] == "weak":
         H = wl["rows"] * N
     else:
         H = wl["rows"]
     W = wl["cols"]
+    if args.grid:  # tests: a small grid through the same machinery
+        H, W = args.grid
     x0, h = mm.partition_rows(H, N, rank)
 
-    if N > 1:
+    ndev = max(1, mm.device_count())
+    dev = local % ndev if host else local
+    if host:
+        eng = mm.Engine(H, W, x0, h, n_attr=wl["n_attr"], device=dev, rank=rank, nranks=N,
+                        halo_mode=mm.MM_HALO_HOST)
+    elif N > 1:
         ids = [mm.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         eng = mm.Engine(H, W, x0, h, n_attr=wl["n_attr"], device=local, rank=rank, nranks=N,
@@ -198,7 +321,14 @@ def main():
                         comm_id_bytes=mm.comm_id())
     else:
         eng = mm.Engine(H, W, n_attr=wl["n_attr"], device=local)
-    sync = lambda: mm.device_synchronize(local)  # noqa: E731
+    sync = lambda: mm.device_synchronize(dev)  # noqa: E731
+    exchange = gloo_exchange(rank, N) if host else None
+
+    def run(n, reduce_every):
+        if host:
+            mm.run_host_halo(eng, n, exchange, reduce_every)
+        else:
+            eng.run(n, reduce_every)
 
     na = wl["n_attr"]
     for a in range(na):
@@ -213,6 +343,7 @@ def main():
     else:
         eng.add_diffuse(0, RATE)
         reduce_every = 0
+
     def global_total(e):
         # total over attributes and ranks: what the flows conserve (src/Model.hpp:95)
         t = torch.tensor([float(sum(e.sums()))], dtype=torch.float64)
@@ -222,10 +353,15 @@ def main():
 
     s_before = global_total(eng)
 
-    # warmup (clocks, caches), then the timed run's one-time work -- its hipGraph capture
-    # and the plan of its eager tail -- done ahead (mm_prepare runs no step)
-    eng.run(args.warmup, reduce_every)
-    eng.prepare(args.steps, reduce_every)
+    # the timed run's one-time work -- its hipGraphs (both buffer parities) and the plan of
+    # its eager passes -- done ahead (mm_prepare runs no step); then the warmup steps, which
+    # end right before the timed region: an idle GPU drops its clock within milliseconds,
+    # and the first ~1 ms of a run after an idle gap is slower (tools/timed_gap.py,
+    # profiles/r03/timed_gap.log: 9.5-9.9 ms for the 20-step run after idle, 8.3-8.4 ms
+    # back to back)
+    if not host:
+        eng.prepare(args.steps, reduce_every)
+    run(args.warmup, reduce_every)
     eng.synchronize()
 
     # timed region: the production path
@@ -233,7 +369,7 @@ def main():
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    eng.run(args.steps, reduce_every)
+    run(args.steps, reduce_every)
     eng.synchronize()
     sync()
     el = time.perf_counter() - t0
@@ -243,6 +379,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     s_after = global_total(eng)
+    if args.dump:  # tests: this rank's slab after warmup + steps
+        import numpy as np
+        np.save(f"{args.dump}.rank{rank}.npy", np.stack([eng.download(a) for a in range(na)]))
 
     # kernel pass: the timed run's own passes (mm_pass_plan), repeated eagerly until at
     # least 3 launches, each step kernel bracketed by HIP events on its stream -- the
@@ -251,26 +390,20 @@ def main():
     reps = max(1, -(-3 // max(len(plan), 1)))
     eng.set_timing(True)
     for _ in range(reps):
-        eng.run(args.steps, reduce_every)
+        run(args.steps, reduce_every)
     n_launch, kern_ms, bytes_per_launch = eng.timing()
     eng.set_timing(False)
-    timing_steps = reps * args.steps
     info = eng.info()
-    if info["graph_state"] == 1:
-        path = f"hipGraph replay ({info['graph_launches']} graph launches)"
-    elif info["graph_state"] == -1:
-        path = f"eager launches: graph capture refused ({info['graph_note']})"
-    else:
-        path = "eager launches (no graph)"
+    passes = [(k, *eng.pass_kernel(k)) for k in plan] * reps
+    gpus = [dev] if N == 1 else None
+    if N > 1:
+        got = [None] * N
+        dist.all_gather_object(got, dev)
+        gpus = got
 
-    cells = H * W
-    gcups = cells * args.steps / el / 1e9
     if rank == 0:
-        kern_avg_ms = kern_ms / max(n_launch, 1)
-        launches_per_step = n_launch / max(timing_steps, 1)
-        spl = max(plan) if info["kernel"] in (2, 3) else 1  # steps of the dominant (longest) pass
+        spl = max(plan) if info["kernel"] in (2, 3) and plan else 1
         kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel", 3: "mm_wide_kernel"}[info["kernel"]]
-        achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         traffic = None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):  # only when it was measured on this kernel
@@ -279,66 +412,12 @@ def main():
             key = f"{args.workload}_n{N}_k{spl}"
             if kname in pmc.get(f"{key}_kernel", ""):
                 traffic = pmc.get(f"{key}_bytes_per_launch")
-        cons = abs(s_after - s_before) / abs(s_before)
-        line = {
-            "metric": "cell-updates/s (GCUPS) per step + % of HBM roofline",
-            "value": round(gcups, 3),
-            "unit": "GCUPS",
-            "n_gpus": N,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el * 1e3 / args.steps, 5),
-            "higher_is_better": True,
-            "scaling": wl["scaling"],
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: v0 = 1 + U[0,1) from splitmix64 keyed by global cell index, "
-                    "seed 0x4D50494D, generated on the device",
-            "config": {"workload": f"{args.workload}: {wl['desc']}", "grid": [H, W],
-                       "path": f"{path}, {kname}, {len(plan)} pass(es) of "
-                               f"{'+'.join(map(str, plan)) if len(plan) <= 8 else f'{spl} (x{len(plan)})'}"
-                               f" fused steps",
-                       "rows_per_gpu": h, "n_attr": na, "rate": RATE,
-                       "parallelism": f"row-slab x{N}" + (" + RCCL halo" if N > 1 else "")
-                       + (" (self-halo: RCCL exchange with itself)" if args.self_halo else ""),
-                       "passes_per_step": info["n_passes"],
-                       "rows_per_wave": info["rows_per_wave"]},
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1) if achieved else None,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic,
-                "kernel": kname,
-                "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "steps_per_launch": spl,
-                "launches_per_step": launches_per_step,
-                # BASELINE.md's formula: GCUPS x 16 B x A / 8 TB/s (per GPU); above 1.0
-                # when K steps share one HBM round trip (temporal blocking)
-                "equivalent_frac": round(gcups / N * 16.0 * na / HBM_PEAK_GBS, 4),
-            },
-            "check": {"total_rel_drift": cons},
-        }
-        if info["kernel"] in (2, 3) and na == 1 and kern_ms > 0 and len(set(plan)) == 1:
-            # the K-step kernels' other roof: the steady-state loop issues,
-            # per level-row of a strip, 7 fp64 VALU instructions per column of a lane (4
-            # cycles per wave on a SIMD) and 4 DPP moves (2 cycles) -- mm_passk_kernel: 2
-            # columns per lane, 128-column strips, 4*ceil(K/2) halo columns; mm_wide_kernel:
-            # 4 columns per lane, 256-column strips, 8*ceil(K/4) halo columns. A launch runs
-            # K levels over every row of ceil(W / output columns) strips (segment overlap,
-            # LDS hand-offs and the edge strips' slower body not counted). frac: those
-            # cycles / the launch's cycles on every SIMD at the 2.4 GHz peak clock. Only
-            # when every pass of the run has the same K (the timed average is one kernel's)
-            cols = 2 if info["kernel"] == 2 else 4
-            oc = 64 * cols - 2 * cols * (-(-spl // cols))
-            level_rows = h * spl * -(-W // oc)
-            cyc = level_rows * (7 * cols * 4 + 4 * 2) / (256 * 4)
-            line["roofline"]["valu"] = {
-                "bound": "valu", "cycles_per_simd_per_launch": round(cyc),
-                "peak_clock_mhz": 2400,
-                "frac": round(cyc / (kern_avg_ms * 1e-3 * 2.4e9), 4)}
+        line = make_line(workload=args.workload, wl=wl, N=N, ranks={"gpus": len(set(gpus))},
+                         H=H, W=W, h=h, na=na, steps=args.steps, warmup=args.warmup, el=el,
+                         plan=plan, info=info, kern_ms=kern_ms, n_launch=n_launch,
+                         timing_steps=reps * args.steps, bytes_per_launch=bytes_per_launch, passes=passes, traffic=traffic,
+                         cons=abs(s_after - s_before) / abs(s_before), halo=args.halo,
+                         self_halo=args.self_halo)
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
                 if na == 1 else cpu_baseline_program(wl["rows"], W, na, C5_FLOWS,

@@ -232,6 +232,11 @@ int mm_prepare(mm_engine* eng, long long nsteps, long long reduce_every);
  * planning, no device work. Replaces nothing in the reference: its time loop
  * (src/Model.hpp:180-183) is commented out. */
 int mm_pass_plan(mm_engine* eng, long long nsteps, int* lens, int cap, int* count);
+/* The kernel a pass of k steps launches (for rooflines): *kernel 0 = one-step
+ * mm_pass_kernel, 2 = mm_passk_kernel, 3 = mm_wide_kernel; *cols_per_lane = columns one
+ * lane computes (2 for mm_passk_kernel, 4 or 8 for mm_wide_kernel); *strips = column
+ * strips of the slab (0 for the one-step kernel). */
+int mm_pass_kernel(mm_engine* eng, int k, int* kernel, int* cols_per_lane, long long* strips);
 int mm_synchronize(mm_engine* eng);
 
 /* Sums of the owned cells. mm_sums reduces the CURRENT state now (synchronous).

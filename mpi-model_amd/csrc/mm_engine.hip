@@ -111,7 +111,8 @@ struct mm_engine {
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
-    int bpc[2][2][mm::kMaxWide + 1] = {};                       // wide kernel blocks/CU cache
+    int bpc[2][2][2][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt][c == 8][k]
+    int wide_cols = 4;  // columns per lane of the wide kernel where it has an instance (MM_WIDE_COLS)
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -238,6 +239,9 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
+// Columns per lane of the wide kernel's k-step instance: 8 where configured and built, else 4.
+int wcols(const mm_engine* e, int k) { return e->wide_cols == 8 && mm::wide_has(k, 8) ? 8 : 4; }
+
 // Launch a one-step pass (kpass == 0), a K-step pass (kpass = K > 0: mm_passk_kernel;
 // kpass = -K: mm_wide_kernel) covering `rows`
 // rows on the compute stream, with an event pair around it when timing. Algorithmic
@@ -256,7 +260,7 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
     if (kpass > 0)
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else if (kpass < 0)
-        MM_HIP(mm::launch_wide(-kpass, red, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), red, A, e->s_comp, e->variant));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -461,11 +465,11 @@ bool wide_on(const mm_engine* e) {
 }
 
 bool use_wide(const mm_engine* e, int k) {
-    return wide_on(e) && e->na == 1 && passk_ok(e) && mm::wide_has(k);
+    return wide_on(e) && e->na == 1 && passk_ok(e) && mm::wide_has(k, wcols(e, k));
 }
 
 long long nstrips_wide(const mm_engine* e, int k) {
-    const int oc = mm::wide_out_cols(k);
+    const int oc = mm::wide_out_cols(k, wcols(e, k));
     return (e->d.W + oc - 1) / oc;
 }
 
@@ -477,8 +481,9 @@ long long nstrips_wide(const mm_engine* e, int k) {
 // profiles/r03/kernel_table).
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
     const int nt = e->variant & 1;
-    int& bpc = e->bpc[red ? 1 : 0][nt][k];
-    if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, red, nt));
+    const int c = wcols(e, k);
+    int& bpc = e->bpc[red ? 1 : 0][nt][c == 8][k];
+    if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, red, nt));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
@@ -538,7 +543,7 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
         B.waves_total = 2 * B.waves_a;
         B.partial_base = interior;
-        MM_HIP(mm::launch_wide(k, red, B, e->s_comm, 0));
+        MM_HIP(mm::launch_wide(k, wcols(e, k), red, B, e->s_comm, 0));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
@@ -1015,9 +1020,11 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
+    if (const char* c = std::getenv("MM_WIDE_COLS")) e->wide_cols = std::atoi(c) == 8 ? 8 : 4;
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
-        if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && mm::wide_has(v)))) e->kpass = v;
+        if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4) || mm::wide_has(v, 8)))))
+            e->kpass = v;
         if (v >= 1) e->kpass_multi = std::min(v, 2);
     }
     if (const char* p = std::getenv("MM_PASS_PLAN")) e->plan = std::atoi(p) != 0;
@@ -1157,9 +1164,10 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         A.nstrips = (int)nstrips_wide(e, spl);
         wide_range(e, spl, false, A, 0, e->d.h);
         info->rows_per_wave = A.th;
-        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl);
+        const int c = wcols(e, spl);
+        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c);
         info->kernel = 3;
-        info->seg_waves_per_cu = e->bpc[0][e->variant & 1][spl] * mm::wide_waves_per_block(spl);
+        info->seg_waves_per_cu = e->bpc[0][e->variant & 1][c == 8][spl] * mm::wide_waves_per_block(spl, c);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);
@@ -1305,9 +1313,10 @@ int check_run(mm_engine* e, long long nsteps, long long reduce_every, const char
     if (e->d.halo_mode == MM_HALO_HOST && e->d.nranks > 1) {
         if (e->passes.size() != 1)
             return fail(MM_ERR_STATE, std::string(who) + ": the host halo transport runs one-pass flow programs only");
-        if (nsteps > halo_depth(e))
-            return fail(MM_ERR_STATE, std::string(who) + ": host halo transport: at most halo_depth steps per "
-                                      "call (exchange halo_depth rows between calls)");
+        // one pass per call: the pass planner's length for nsteps (<= kGhost rows exchanged)
+        if (nsteps > mm::kGhost || (passk_ok(e) ? next_pass_len(e, nsteps) : 1) != nsteps)
+            return fail(MM_ERR_STATE, std::string(who) + ": host halo transport: one pass per call "
+                                      "(mm_pass_plan's pass lengths; exchange that many rows between calls)");
     }
     return MM_OK;
 }
@@ -1329,18 +1338,25 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
     const long long per = e->timing ? 0 : graph_per(e, nsteps, reduce_every);
     long long tail = nsteps;
     if (per > 0) {
-        hipGraphExec_t g = nullptr;
-        int flip = 0;
-        if (get_graph(e, per, reduce_every, phase, &g, &flip) != MM_OK) {
-            e->graph_note = g_last_error;
-            (void)hipGetLastError();
-            e->graphs_ok = false;
-            e->graph_state = -1;
-        } else {
-            MM_HIP(hipGraphUpload(g, e->s_comp));  // the first launch then uploads nothing
-            MM_HIP(hipStreamSynchronize(e->s_comp));
-            tail = nsteps % per;
+        // both buffer parities: untimed warmup steps run after mm_prepare may leave the
+        // state at either one (graphs are keyed by the parity they start from)
+        const int cur0 = e->cur;
+        for (int par = 0; par < 2 && e->graphs_ok; ++par) {
+            e->cur = cur0 ^ par;
+            hipGraphExec_t g = nullptr;
+            int flip = 0;
+            if (get_graph(e, per, reduce_every, phase, &g, &flip) != MM_OK) {
+                e->graph_note = g_last_error;
+                (void)hipGetLastError();
+                e->graphs_ok = false;
+                e->graph_state = -1;
+            } else {
+                MM_HIP(hipGraphUpload(g, e->s_comp));  // the first launch then uploads nothing
+                tail = nsteps % per;
+            }
         }
+        e->cur = cur0;
+        MM_HIP(hipStreamSynchronize(e->s_comp));
     }
     // the eagerly launched passes: plan them now, which loads their kernels' code objects
     if (passk_ok(e) && tail > 0) {
@@ -1375,6 +1391,26 @@ int mm_pass_plan(mm_engine* e, long long nsteps, int* lens, int cap, int* count)
             if (n < cap) lens[n] = 1;
     }
     *count = n;
+    return MM_OK;
+}
+
+int mm_pass_kernel(mm_engine* e, int k, int* kernel, int* cols_per_lane, long long* strips) {
+    if (!e || k < 1 || !kernel || !cols_per_lane || !strips)
+        return fail(MM_ERR_INVALID, "mm_pass_kernel: bad arguments");
+    if (e->passes.empty()) return fail(MM_ERR_STATE, "mm_pass_kernel: no flow added (mm_add_flow)");
+    if (!passk_ok(e)) {  // one mm_pass_kernel launch per pass of the step
+        *kernel = 0;
+        *cols_per_lane = 1;
+        *strips = 0;
+    } else if (use_wide(e, k)) {
+        *kernel = 3;
+        *cols_per_lane = wcols(e, k);
+        *strips = nstrips_wide(e, k);
+    } else {
+        *kernel = 2;
+        *cols_per_lane = 2;
+        *strips = nstrips_k(e, k);
+    }
     return MM_OK;
 }
 

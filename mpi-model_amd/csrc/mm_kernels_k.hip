@@ -91,15 +91,24 @@ hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t 
     }
 }
 
-bool wide_has(int k) { return k == 4 || k == 8 || k == 12 || k == 16 || k == 20; }
-
-int wide_out_cols(int k) {
-    return kWideStrip - 2 * kWideCols * ((k + kWideCols - 1) / kWideCols);
+bool wide_has(int k, int c) {
+    if (c == 8) return k == 8 || k == 12 || k == 16;
+    return c == 4 && (k == 4 || k == 8 || k == 12 || k == 16 || k == 20);
 }
 
-int wide_waves_per_block(int k) { return wide_has(k) ? 4 : 0; }
+int wide_out_cols(int k, int c) { return 64 * c - 2 * c * ((k + c - 1) / c); }
 
-int wide_blocks_per_cu(int k, bool red, int nt) {
+int wide_waves_per_block(int k, int c) { return wide_has(k, c) ? 4 : 0; }
+
+int wide_blocks_per_cu(int k, int c, bool red, int nt) {
+    if (c == 8) {
+        switch (k) {
+            case 8: return wide8_blocks_k8(red, nt);
+            case 12: return wide8_blocks_k12(red, nt);
+            case 16: return wide8_blocks_k16(red, nt);
+            default: return 0;
+        }
+    }
     switch (k) {
         case 4: return wide_blocks_k4(red, nt);
         case 8: return wide_blocks_k8(red, nt);
@@ -110,8 +119,16 @@ int wide_blocks_per_cu(int k, bool red, int nt) {
     }
 }
 
-hipError_t launch_wide(int k, bool red, const PassArgs& a, hipStream_t s, int variant) {
+hipError_t launch_wide(int k, int c, bool red, const PassArgs& a, hipStream_t s, int variant) {
     if (a.waves_total <= 0) return hipSuccess;
+    if (c == 8) {
+        switch (k) {
+            case 8: return wide8_launch_k8(red, a, s, variant);
+            case 12: return wide8_launch_k12(red, a, s, variant);
+            case 16: return wide8_launch_k16(red, a, s, variant);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (k) {
         case 4: return wide_launch_k4(red, a, s, variant);
         case 8: return wide_launch_k8(red, a, s, variant);

@@ -29,7 +29,7 @@ EXPORTS = [
     "mm_owner_reference", "mm_partition_rows", "mm_neighbor_count", "mm_comm_id_size",
     "mm_comm_id_create", "mm_device_count", "mm_device_synchronize", "mm_engine_create", "mm_engine_destroy",
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
-    "mm_point_apply", "mm_run", "mm_prepare", "mm_pass_plan", "mm_synchronize", "mm_sums", "mm_sums_history",
+    "mm_point_apply", "mm_run", "mm_prepare", "mm_pass_plan", "mm_pass_kernel", "mm_synchronize", "mm_sums", "mm_sums_history",
     "mm_clear_history", "mm_halo_export_rows", "mm_halo_import_rows", "mm_halo_export",
     "mm_halo_import", "mm_debug_read_rows",
     "mm_set_timing", "mm_timing", "mm_partition_rect_reference", "mm_owner_rect_reference",
@@ -102,6 +102,7 @@ def lib():
             "mm_run": (I, [P, LL, LL]),
             "mm_prepare": (I, [P, LL, LL]),
             "mm_pass_plan": (I, [P, LL, pI, I, pI]),
+            "mm_pass_kernel": (I, [P, I, pI, pI, pLL]),
             "mm_synchronize": (I, [P]),
             "mm_sums": (I, [P, P]),
             "mm_sums_history": (I, [P, P, LL, pLL]),
@@ -224,6 +225,24 @@ def device_count():
     return n.value
 
 
+def run_host_halo(eng, nsteps, exchange, reduce_every=0):
+    """nsteps steps of a MM_HALO_HOST slab in a chain of ranks: before every K-step pass of
+    the engine's plan (mm_pass_plan) the slab's first / last K rows go out and the
+    neighbours' K rows come in (`exchange(top, bottom, k) -> (above, below)`, None where the
+    slab has no neighbour), then the pass runs. Every rank's plan is the same (it is sized
+    by the chain's thinnest slab), so the exchanges pair up."""
+    single = {}
+    for k in eng.pass_plan(nsteps):
+        if k not in single:  # a k-step run is exactly one k-step pass
+            single[k] = eng.pass_plan(k) == [k]
+            if not single[k]:
+                raise RuntimeError(f"run_host_halo: a {k}-step run is not one pass")
+        top, bottom = eng.halo_export(k)
+        above, below = exchange(top, bottom, k)
+        eng.halo_import(above, below, nrows=k)
+        eng.run(k, reduce_every)
+
+
 class Engine:
     """One row slab [x_init, x_init+h) of an H x W grid on one GPU."""
 
@@ -314,6 +333,14 @@ class Engine:
         buf = (ctypes.c_int * max(cnt.value, 1))()
         check(lib().mm_pass_plan(self.ptr, nsteps, buf, cnt.value, ctypes.byref(cnt)))
         return list(buf[:cnt.value])
+
+    def pass_kernel(self, k):
+        """(kernel, columns per lane, strips) of a k-step pass (mm_pass_kernel): kernel 0 =
+        mm_pass_kernel, 2 = mm_passk_kernel, 3 = mm_wide_kernel."""
+        kern, cols, strips = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
+        check(lib().mm_pass_kernel(self.ptr, k, ctypes.byref(kern), ctypes.byref(cols),
+                                   ctypes.byref(strips)))
+        return kern.value, cols.value, strips.value
 
     def synchronize(self):
         check(lib().mm_synchronize(self.ptr))

@@ -196,7 +196,11 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}]
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}] + [
+    # the 8-column instances (ascending levels, no pend registers)
+    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": k} for k in (8, 12, 16)] + [
+    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
+    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": 16, "MM_XCD_REMAP": 1}]
 
 
 def env_id(env):
@@ -238,7 +242,9 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
                                  {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
                                  {"MM_STEPS_PER_PASS": 7},
                                  {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}]
-                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)]
+                         + [{"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": k}
+                            for k in (8, 12, 16)],
                          ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
@@ -265,13 +271,14 @@ def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
 
 
 @pytest.mark.parametrize("k,wide", [(k, 0) for k in (2, 3, 4, 6, 7, 8, 9, 10)]
-                         + [(k, 1) for k in (4, 8, 12, 16, 20)])
+                         + [(k, 1) for k in (4, 8, 12, 16, 20)] + [(k, 8) for k in (8, 12, 16)])
 def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k, wide):
     # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
     # multiple of the graph length, so the tail runs eagerly (K >= 10: a graph holds
     # 6K steps -- an even number of flips and whole reduction periods -- so run 13K)
     H, W, steps = 300, 700, (50 if k < 10 else 13 * k)
-    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k, MM_WIDE=wide)
+    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k, MM_WIDE=int(wide > 0),
+                        MM_WIDE_COLS=8 if wide == 8 else 4)
     e.fill_random(0)
     e.add_diffuse(0, 0.2)
     e.run(steps, 3)

@@ -2,7 +2,8 @@
 """HIP-event time of one K-step pass per grid size and kernel (mm_passk_kernel at K, or
 mm_wide_kernel at K), the table the pass planner's cost model is fitted to.
 
-  python tools/kernel_table.py --sizes 32768x32768,16384x16384 --old 7,8,10 --wide 8,12,16,20
+  python tools/kernel_table.py --sizes 32768x32768,16384x16384 --old 7,8,10 --wide 8,12,16,20 \
+      --wide8 8,12,16
 """
 import argparse
 import json
@@ -16,8 +17,9 @@ import mpimodel as mm  # noqa: E402
 mm.lib()
 
 
-def one(H, W, k, wide, reps):
-    env = {"MM_STEPS_PER_PASS": str(k), "MM_WIDE": "1" if wide else "0"}
+def one(H, W, k, wide, reps, cols=4):
+    env = {"MM_STEPS_PER_PASS": str(k), "MM_WIDE": "1" if wide else "0",
+           "MM_WIDE_COLS": str(cols)}
     old = {key: os.environ.get(key) for key in env}
     os.environ.update(env)
     try:
@@ -36,9 +38,10 @@ def one(H, W, k, wide, reps):
     n, ms, _ = e.timing()
     e.set_timing(False)
     info = e.info()
+    kern, c, strips = e.pass_kernel(k)
     e.close()
     us = ms / n * 1e3
-    return {"H": H, "W": W, "k": k, "kernel": info["kernel"], "pass_us": round(us, 1),
+    return {"H": H, "W": W, "k": k, "kernel": kern, "cols": c, "strips": strips, "pass_us": round(us, 1),
             "us_per_step": round(us / k, 2), "GCUPS": round(H * W * k / us / 1e3, 1),
             "rows_per_wave": info["rows_per_wave"], "waves": info["waves_per_pass"]}
 
@@ -48,6 +51,7 @@ def main():
     ap.add_argument("--sizes", default="32768x32768,16384x16384,8192x32768,4096x32768,4096x4096")
     ap.add_argument("--old", default="7,8,10")
     ap.add_argument("--wide", default="4,8,12,16,20")
+    ap.add_argument("--wide8", default="", help="K of the 8-column wide instances")
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     for sz in a.sizes.split(","):
@@ -56,6 +60,8 @@ def main():
             print(json.dumps(one(H, W, k, False, a.reps)), flush=True)
         for k in [int(x) for x in a.wide.split(",") if x]:
             print(json.dumps(one(H, W, k, True, a.reps)), flush=True)
+        for k in [int(x) for x in a.wide8.split(",") if x]:
+            print(json.dumps(one(H, W, k, True, a.reps, cols=8)), flush=True)
 
 
 if __name__ == "__main__":
