@@ -111,8 +111,7 @@ struct mm_engine {
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
-    int bpc[2][2][2][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt][c == 8][k]
-    int wide_cols = 4;  // columns per lane of the wide kernel where it has an instance (MM_WIDE_COLS)
+    int bpc[2][2][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt][k]
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -239,8 +238,8 @@ hipEvent_t next_event(mm_engine* e) {
     return e->ev_pool[e->ev_used++];
 }
 
-// Columns per lane of the wide kernel's k-step instance: 8 where configured and built, else 4.
-int wcols(const mm_engine* e, int k) { return e->wide_cols == 8 && mm::wide_has(k, 8) ? 8 : 4; }
+// Columns per lane of the wide kernel: 4 for one attribute, 2 for several.
+int wcols(const mm_engine* e, int) { return e->na > 1 ? 2 : 4; }
 
 // Launch a one-step pass (kpass == 0), a K-step pass (kpass = K > 0: mm_passk_kernel;
 // kpass = -K: mm_wide_kernel) covering `rows`
@@ -260,7 +259,7 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
     if (kpass > 0)
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else if (kpass < 0)
-        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), red, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp, e->variant));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -460,12 +459,15 @@ bool passk_ok(const mm_engine* e);
 constexpr double kWideCells = 268435456.0;  // 2^28: 16384^2, 8192 x 32768 and up
 
 bool wide_on(const mm_engine* e) {
-    // auto: sized by the chain's thinnest slab (rank-invariant, like every plan input)
-    return e->wide > 0 || (e->wide < 0 && (double)e->min_rows * (double)e->d.W >= kWideCells);
+    // auto: several attributes always (K = 8 instead of mm_passk_kernel's 2); one attribute
+    // on slabs of >= kWideCells cells, sized by the chain's thinnest slab (rank-invariant,
+    // like every plan input)
+    return e->wide > 0 ||
+           (e->wide < 0 && (e->na > 1 || (double)e->min_rows * (double)e->d.W >= kWideCells));
 }
 
 bool use_wide(const mm_engine* e, int k) {
-    return wide_on(e) && e->na == 1 && passk_ok(e) && mm::wide_has(k, wcols(e, k));
+    return wide_on(e) && passk_ok(e) && mm::wide_has(k, wcols(e, k), e->na);
 }
 
 long long nstrips_wide(const mm_engine* e, int k) {
@@ -482,8 +484,8 @@ long long nstrips_wide(const mm_engine* e, int k) {
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
     const int nt = e->variant & 1;
     const int c = wcols(e, k);
-    int& bpc = e->bpc[red ? 1 : 0][nt][c == 8][k];
-    if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, red, nt));
+    int& bpc = e->bpc[red ? 1 : 0][nt][k];
+    if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, e->na, red, nt));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
@@ -543,7 +545,7 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
         B.waves_total = 2 * B.waves_a;
         B.partial_base = interior;
-        MM_HIP(mm::launch_wide(k, wcols(e, k), red, B, e->s_comm, 0));
+        MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, 0));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
@@ -627,7 +629,8 @@ bool passk_ok(const mm_engine* e) {
     return true;
 }
 
-constexpr int kWideAuto = 16;  // auto steps per pass of the wide kernel
+constexpr int kWideAuto = 16;      // auto steps per pass of the wide kernel, one attribute
+constexpr int kWideAutoMulti = 8;  // several attributes
 
 // Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
 // past the thinnest slab of the chain (every rank sends K owned rows each way).
@@ -645,6 +648,11 @@ int passk_steps(const mm_engine* e) {
     int k1 = e->kpass > 0 ? e->kpass : kauto;
     if (!(wide_on(e) && e->na == 1)) k1 = std::min(k1, mm::kMaxSteps);  // mm_passk_kernel's K
     int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
+    // several attributes, wide kernel: its K (auto kWideAutoMulti), or mm_passk_kernel's
+    if (e->na > 1 && wide_on(e) && passk_ok(e)) {
+        k = e->kpass > 0 ? e->kpass : kWideAutoMulti;
+        if (!mm::wide_has(k, 2, e->na)) k = std::min(k, mm::passk_max_steps(e->na));
+    }
     if (e->d.nranks > 1) k = (int)std::min<long long>(k, e->min_rows);
     return std::max(1, k);
 }
@@ -676,7 +684,7 @@ double pass_cost(int k) {
 // (1000 steps: 125 passes).
 // A pass of k steps has a kernel: the wide one (use_wide) or mm_passk_kernel (k <= 10).
 bool pass_len_ok(const mm_engine* e, long long k) {
-    return k >= 1 && (k <= mm::kMaxSteps || use_wide(e, (int)k));
+    return k >= 1 && (k <= mm::passk_max_steps(e->na) || use_wide(e, (int)k));
 }
 
 // Modelled time of one k-step pass on a large slab with the wide kernel on (HIP-event pass
@@ -720,6 +728,11 @@ int wide_plan_first(const mm_engine* e, long long n, int kcap) {
 
 int next_pass_len(const mm_engine* e, long long n) {
     const int kp = passk_steps(e);
+    if (e->na > 1 && wide_on(e)) {  // passes of K while n >= K, then the longest that fit
+        long long k = std::min<long long>(n, kp);
+        while (k > 1 && !pass_len_ok(e, k)) --k;
+        return (int)std::max<long long>(1, k);
+    }
     if (wide_on(e) && e->na == 1) {
         if (e->kpass == 0 && e->plan) {
             int cap = mm::kMaxWide;
@@ -875,7 +888,7 @@ int ensure_partials(mm_engine* e) {
     const long long ns = nstrips_k(e, mm::kMaxSteps);
     const long long border = 2 * ((mm::kGhost + mm::kBorderRows - 1) / mm::kBorderRows) + 2;
     need = std::max(need, (ns * ((e->d.h + 7) / 8 + border) + 16) *
-                              std::max(mm::kMaxWide, 2 * mm::kMaxAttr));
+                              std::max(mm::kMaxWide, 8 * mm::kMaxAttr));
     if (need <= e->partials_cap) return MM_OK;
     if (e->partials) (void)hipFree(e->partials);
     e->partials = nullptr;
@@ -894,8 +907,9 @@ int reserve_history(mm_engine* e, long long more) {
     MM_HIP(hipStreamSynchronize(e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comm));
     MM_HIP(hipMalloc(&nh, sizeof(double) * (size_t)cap * e->na));
-    MM_HIP(hipMemcpy(nh, e->hist, sizeof(double) * (size_t)e->hist_cap * e->na,
-                     hipMemcpyDeviceToDevice));
+    MM_HIP(hipMemcpyAsync(nh, e->hist, sizeof(double) * (size_t)e->hist_cap * e->na,
+                          hipMemcpyDeviceToDevice, e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
     (void)hipFree(e->hist);
     e->hist = nh;
     e->hist_cap = cap;
@@ -1020,10 +1034,9 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
-    if (const char* c = std::getenv("MM_WIDE_COLS")) e->wide_cols = std::atoi(c) == 8 ? 8 : 4;
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
-        if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4) || mm::wide_has(v, 8)))))
+        if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4, 1) || mm::wide_has(v, 2, 4)))))
             e->kpass = v;
         if (v >= 1) e->kpass_multi = std::min(v, 2);
     }
@@ -1080,6 +1093,11 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     e->sum_blocks = std::min<long long>(1024, std::max<long long>(1, d.h));
     if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "sum scratch allocation failed"));
+    // the zeroing above runs on the null stream, which the engine's non-blocking streams do
+    // not wait for: without this a fill (or a history append) could land before it and be
+    // zeroed -- it did, on memory another engine had just freed (tools/dbg_chain2.py)
+    he = hipDeviceSynchronize();
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipDeviceSynchronize: ") + hipGetErrorString(he)));
 
     if (const char* sh = std::getenv("MM_SELF_HALO"))
         e->self_halo = d.nranks == 1 && d.halo_mode == MM_HALO_RCCL && std::atoi(sh) != 0;
@@ -1165,9 +1183,10 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         wide_range(e, spl, false, A, 0, e->d.h);
         info->rows_per_wave = A.th;
         const int c = wcols(e, spl);
-        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c);
+        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na);
         info->kernel = 3;
-        info->seg_waves_per_cu = e->bpc[0][e->variant & 1][c == 8][spl] * mm::wide_waves_per_block(spl, c);
+        info->seg_waves_per_cu =
+            e->bpc[0][e->variant & 1][spl] * mm::wide_waves_per_block(spl, c, e->na);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);
@@ -1503,7 +1522,8 @@ int mm_clear_history(mm_engine* e) {
     if (!e) return fail(MM_ERR_INVALID, "mm_clear_history: null");
     MM_TRY(set_device(e));
     MM_HIP(hipStreamSynchronize(e->s_comp));
-    MM_HIP(hipMemset(e->hist_n, 0, sizeof(unsigned long long)));
+    MM_HIP(hipMemsetAsync(e->hist_n, 0, sizeof(unsigned long long), e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
     e->hist_host = 0;
     return MM_OK;
 }

@@ -61,17 +61,18 @@ int passk_max_steps(int na);
 long long passk_max_rows(int k, long long pitch);
 // resident waves per CU of the segment kernel (occupancy API), 0 if unknown
 int passk_waves_per_cu(int k, int na, bool red, int nt);
-// Level-split K-step kernel (mm_wide_kernel, one attribute, one diffusion) with c columns
-// per lane: c = 4 for K in {4, 8, 12, 16, 20}, c = 8 for K in {8, 12, 16}; one workgroup of
-// wide_waves_per_block(k, c) waves per strip segment, segment schedule only (a.seg; a.th /
-// a.th_edge rows per block, a.waves_a / a.waves_total count BLOCKS), a.nstrips =
-// ceil(W / wide_out_cols(k, c)). red: every level's sums into partials[block][k]. variant
-// bit 0: non-temporal stores.
-bool wide_has(int k, int c);
+// Level-split K-step kernel (mm_wide_kernel) of a one-pass program with na attributes and
+// c columns per lane: na = 1 (one diffusion) with c = 4 for K in {4, 8, 12, 16, 20}; na = 4 (transfer chains + diffusions, config C5) with c = 2 for K in
+// {4, 8}. One workgroup of wide_waves_per_block(k, c, na) waves per strip segment, segment
+// schedule only (a.seg; a.th / a.th_edge rows per block, a.waves_a / a.waves_total count
+// BLOCKS), a.nstrips = ceil(W / wide_out_cols(k, c)). red: every level's sums into
+// partials[block][k][na]. variant bit 0: non-temporal stores.
+bool wide_has(int k, int c, int na);
 int wide_out_cols(int k, int c);
-int wide_waves_per_block(int k, int c);
-int wide_blocks_per_cu(int k, int c, bool red, int nt);
-hipError_t launch_wide(int k, int c, bool red, const PassArgs& a, hipStream_t s, int variant);
+int wide_waves_per_block(int k, int c, int na);
+int wide_blocks_per_cu(int k, int c, int na, bool red, int nt);
+hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
+                       int variant);
 // Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k][na],
 // each summed in a fixed order, to the history (na sums per entry).
 hipError_t launch_finalize_levels(const double* partials, long long n, int k, int na, int mask,

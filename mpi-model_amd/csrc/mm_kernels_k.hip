@@ -91,51 +91,43 @@ hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t 
     }
 }
 
-bool wide_has(int k, int c) {
-    if (c == 8) return k == 8 || k == 12 || k == 16;
+bool wide_has(int k, int c, int na) {
+    if (na > 1) return na == 4 && c == 2 && (k == 4 || k == 8);
     return c == 4 && (k == 4 || k == 8 || k == 12 || k == 16 || k == 20);
 }
 
 int wide_out_cols(int k, int c) { return 64 * c - 2 * c * ((k + c - 1) / c); }
 
-int wide_waves_per_block(int k, int c) { return wide_has(k, c) ? 4 : 0; }
+int wide_waves_per_block(int k, int c, int na) {
+    if (!wide_has(k, c, na)) return 0;
+    return na > 1 && k == 8 ? 8 : 4;  // mm_widea_k8: one level per wave
+}
 
-int wide_blocks_per_cu(int k, int c, bool red, int nt) {
-    if (c == 8) {
-        switch (k) {
-            case 8: return wide8_blocks_k8(red, nt);
-            case 12: return wide8_blocks_k12(red, nt);
-            case 16: return wide8_blocks_k16(red, nt);
-            default: return 0;
-        }
-    }
+int wide_blocks_per_cu(int k, int c, int na, bool red, int nt) {
+    if (!wide_has(k, c, na)) return 0;
+    if (na > 1) return k == 4 ? widea_blocks_k4(na, red, nt) : widea_blocks_k8(na, red, nt);
     switch (k) {
         case 4: return wide_blocks_k4(red, nt);
         case 8: return wide_blocks_k8(red, nt);
         case 12: return wide_blocks_k12(red, nt);
         case 16: return wide_blocks_k16(red, nt);
-        case 20: return wide_blocks_k20(red, nt);
-        default: return 0;
+        default: return wide_blocks_k20(red, nt);
     }
 }
 
-hipError_t launch_wide(int k, int c, bool red, const PassArgs& a, hipStream_t s, int variant) {
+hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
+                       int variant) {
     if (a.waves_total <= 0) return hipSuccess;
-    if (c == 8) {
-        switch (k) {
-            case 8: return wide8_launch_k8(red, a, s, variant);
-            case 12: return wide8_launch_k12(red, a, s, variant);
-            case 16: return wide8_launch_k16(red, a, s, variant);
-            default: return hipErrorInvalidValue;
-        }
-    }
+    if (!wide_has(k, c, na)) return hipErrorInvalidValue;
+    if (na > 1)
+        return k == 4 ? widea_launch_k4(na, red, a, s, variant)
+                      : widea_launch_k8(na, red, a, s, variant);
     switch (k) {
         case 4: return wide_launch_k4(red, a, s, variant);
         case 8: return wide_launch_k8(red, a, s, variant);
         case 12: return wide_launch_k12(red, a, s, variant);
         case 16: return wide_launch_k16(red, a, s, variant);
-        case 20: return wide_launch_k20(red, a, s, variant);
-        default: return hipErrorInvalidValue;
+        default: return wide_launch_k20(red, a, s, variant);
     }
 }
 

@@ -14,21 +14,28 @@
 // thrown away. Here a workgroup of P waves shares ONE strip: wave p runs levels
 // p*KW+1 .. (p+1)*KW and hands its last level's rows to wave p+1 through a double-buffered
 // LDS ring, one workgroup barrier per group of B rows. Each wave holds only KW levels, so a
-// lane holds C = 4 or 8 columns (one strip = 64*C loaded columns, C/2 16-B loads per lane
-// and row): a level-row of a lane is 7*C fp64 operations and 4 DPP moves, and the halo --
-// ceil(K/C) lanes per side -- is 16 / 256 columns per side at K = 16 with C = 4, 16 / 512
-// with C = 8.
+// lane holds C = 4 columns (one strip = 256 loaded columns, two 16-B loads per lane and
+// row): a level-row of a lane is 28 fp64 operations and 4 DPP moves (2 per column at
+// C = 2), and the halo -- ceil(K/4) lanes per side -- is 16 / 256 columns per side at
+// K = 16 instead of 10 / 128 at K = 10.
 //
-// C = 4 runs two waves per SIMD (<= 256 VGPRs: KW <= 4 levels of 4 columns); C = 8 holds
-// twice the state per level and runs ONE wave per SIMD (<= 512 VGPRs; MW = 1), one
-// workgroup per CU -- the level chains of 8 columns give the single wave enough
-// independent instructions to keep its SIMD busy.
+// Several attributes (config C5: four, with same-cell transfer chains before / after the
+// diffusions) hold NA windows per level: C = 2 columns per lane keeps the state of a level
+// near a one-attribute level's at C = 4 (NA * C doubles per cell row).
+//
+// C = 8 columns per lane (KW <= 3 levels at <= 256 VGPRs: gfx950's arch VGPRs stop at 256
+// per wave, the rest of the 512-entry file is AGPRs that VALU operations cannot read) was
+// built and measured at 2.5x the time of C = 4 whether its levels were ordered with the
+// pend hand-off or ascending, and 1.75x with deeper prefetch at one workgroup per CU
+// (profiles/r03/r3d, profiles/r03/var). Not diagnosed further (a suspect: with a 64-B slice
+// per lane every 16-B load instruction touches 64 lines a quarter each); not instantiated.
 //
 // Pipeline (the skew of mm_passk.hpp, across waves): level j's m-th input row arrives at
 // iteration m + 3(j-1) and it emits one row per input from its third input on; level j's
 // output of iteration i is level j+1's input at iteration i+1 -- in registers inside a
-// wave (MM_WIDE_ASC: at iteration i, skew 2), through LDS between waves. Wave p's levels start at iteration p*D; before that it
-// only joins the barriers, so every wave passes the same number of barriers. Wave 0
+// wave (MM_WIDE_ASC: at iteration i, skew 2; 0.6 % slower at K = 16), through LDS between
+// waves. Wave p's levels start at iteration p*D; before that it only joins the barriers,
+// so every wave passes the same number of barriers. Wave 0
 // streams the input rows from HBM (U rows prefetched); wave P-1 stores level K's rows.
 //
 // Columns: lane l holds columns c0+C*l .. c0+C*l+C-1. DPP wave_shr / wave_shl give the
@@ -43,7 +50,7 @@
 
 namespace mm {
 
-// per-(K, C) entry points (mm_wide_k*.hip: C = 4, mm_wide8_k*.hip: C = 8)
+// per-K entry points (mm_wide_k*.hip: one attribute, C = 4)
 #define MM_WIDE_DECL(K)                                                                    \
     hipError_t wide_launch_k##K(bool red, const PassArgs& a, hipStream_t s, int v);       \
     int wide_blocks_k##K(bool red, int nt);
@@ -53,13 +60,13 @@ MM_WIDE_DECL(12)
 MM_WIDE_DECL(16)
 MM_WIDE_DECL(20)
 #undef MM_WIDE_DECL
-#define MM_WIDE8_DECL(K)                                                                   \
-    hipError_t wide8_launch_k##K(bool red, const PassArgs& a, hipStream_t s, int v);      \
-    int wide8_blocks_k##K(bool red, int nt);
-MM_WIDE8_DECL(8)
-MM_WIDE8_DECL(12)
-MM_WIDE8_DECL(16)
-#undef MM_WIDE8_DECL
+// several attributes (mm_widea_k*.hip): 2 columns per lane
+#define MM_WIDEA_DECL(K)                                                                   \
+    hipError_t widea_launch_k##K(int na, bool red, const PassArgs& a, hipStream_t s, int v); \
+    int widea_blocks_k##K(int na, bool red, int nt);
+MM_WIDEA_DECL(4)
+MM_WIDEA_DECL(8)
+#undef MM_WIDEA_DECL
 
 namespace {
 
@@ -216,72 +223,191 @@ struct WGeom {
     static constexpr int T0 = (S0 + B - 1) / B * B;  // wave 0: compile-time iterations
 };
 
-// Per-wave constants of one block.
-template <int C>
+// Per-wave constants of one block (NA attributes).
+template <int C, int NA>
 struct WCtx {
     WLane<C> c;
     int p, lane, rA, rB;
     int start;            // first iteration of this wave (p * D)
+    int dmask;            // bit a: attribute a diffuses (NA > 1)
     long long g0;         // global row of input row 0 (rA - K)
-    double r, r8;
+    double r[NA], r8[NA];
     unsigned voff, soff, rowb;
-    __amdgpu_buffer_rsrc_t in, out;
-    dv2* lds_in;          // stage p-1 (RL row slots of 32*C dv2)
+    __amdgpu_buffer_rsrc_t in[NA], out[NA];
+    dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
     double* partials;
     long long pbase;
+    const PassArgs* A;    // transfer chains (NA > 1)
 };
 
-template <int C, int KW, int U>
+template <int C, int NA, int KW, int U>
 struct WState {
-    WinC<C> win[KW];
-    double pend[KW][C];    // pend[q]: level q's row of the previous iteration (q < KW-1)
-    dv2 raw[U][C / 2];     // first wave: prefetched input rows
-    double acc[KW];
+    WinC<C> win[KW][NA];
+    double pend[KW][NA][C];  // pend[q]: level q's row of the previous iteration (q < KW-1)
+    dv2 raw[U][NA][C / 2];   // first wave: prefetched input rows
+    double acc[KW][NA];
 };
+
+#ifndef MM_CHAIN_BRANCH
+#define MM_CHAIN_BRANCH 1  // transfer operands picked by scalar branches (0: chain_k's indexing)
+#endif
+
+// A transfer chain in declared order (oracle/mm_oracle.c, chain_k) on each of this lane's C
+// cells: out = r*u_a; u_a -= out; u_b += out (b < 0: the outflow leaves the system). a and
+// b are wave-uniform kernel arguments, so a scalar branch per transfer and operand picks
+// the attribute's registers: 3 fp64 operations per transfer and cell, where chain_k's
+// register-vector indexing (s_set_gpr_idx) adds two moves per operand access. The empty
+// asm keeps each case a branch (no speculation of the other attributes' cases into selects).
+template <int C, int NA>
+__device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const signed char* ta,
+                                           const signed char* tb, const double* tr) {
+#if MM_CHAIN_BRANCH
+#pragma unroll
+    for (int t = 0; t < kMaxChain; ++t) {
+        if (t >= n) break;  // wave-uniform
+        const int a = __builtin_amdgcn_readfirstlane((int)ta[t]);
+        const int b = __builtin_amdgcn_readfirstlane((int)tb[t]);
+        const double r = tr[t];
+        double out[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) out[k] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            if (a == q) {
+                asm volatile("");
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    out[k] = r * u[q][k];
+                    u[q][k] = u[q][k] - out[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            if (b == q) {
+                asm volatile("");
+#pragma unroll
+                for (int k = 0; k < C; ++k) u[q][k] = u[q][k] + out[k];
+            }
+        }
+    }
+#else
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        double v[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) v[a] = u[a][k];
+        chain_k<NA>(v, n, ta, tb, tr);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) u[a][k] = v[a];
+    }
+#endif
+}
+
+// One level, input m = 0 / 1: the pre-chain (NA > 1), then every attribute's window; an
+// attribute that does not diffuse in this pass emits nothing (s = 0, d = u).
+template <int C, int NA, int BODY>
+__device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
+                                      WinC<C> (&w)[NA], double (&u)[NA][C]) {
+    if (NA > 1 && x.A->npre) chain_cols<C, NA>(u, x.A->npre, x.A->pre_a, x.A->pre_b, x.A->pre_r);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        if (NA > 1 && !((x.dmask >> a) & 1)) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                if (m == 0) {
+                    w[a].sp[k] = 0.0;
+                } else {
+                    w[a].sc[k] = 0.0;
+                    w[a].dc[k] = u[a][k];
+                }
+            }
+        } else {
+            wfill<C, BODY>(x.c, x.r[a], x.r8[a], gx, m, w[a], u[a]);
+        }
+    }
+}
+
+// One level, input m >= 2: the pre-chain, every attribute's emitted row, the post-chain
+// (oracle/mm_oracle.c or_program_step's order within a pass).
+template <int C, int NA, int BODY>
+__device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C> (&w)[NA],
+                                      double (&u)[NA][C], double (&o)[NA][C]) {
+    if (NA > 1 && x.A->npre) chain_cols<C, NA>(u, x.A->npre, x.A->pre_a, x.A->pre_b, x.A->pre_r);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        if (NA > 1 && !((x.dmask >> a) & 1)) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                o[a][k] = w[a].dc[k];
+                w[a].sp[k] = w[a].sc[k];
+                w[a].sc[k] = 0.0;
+                w[a].dc[k] = u[a][k];
+            }
+        } else {
+            wemit<C, BODY>(x.c, x.r[a], x.r8[a], gx, w[a], u[a], o[a]);
+        }
+    }
+    if (NA > 1 && x.A->npost)
+        chain_cols<C, NA>(o, x.A->npost, x.A->post_a, x.A->post_b, x.A->post_r);
+}
 
 // One iteration i of a wave (local iteration t = i - start): input row -> its KW levels
 // (descending, so pend[q-1] is read before level q-1 refills it; ascending with
 // MM_WIDE_ASC) -> level KW-1's row to LDS or HBM. PRO: t is a prologue iteration known at
 // compile time (level q takes part from t = kSkew*q and emits from t = kSkew*q + 2);
 // otherwise every level emits. slot: ring slot (first wave, compile time after unrolling).
-template <int C, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE, bool PRO>
-__device__ __forceinline__ void wave_iter(const WCtx<C>& x, WState<C, KW, U>& st, int i, int t,
-                                          int slot) {
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE,
+          bool PRO>
+__device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st, int i,
+                                          int t, int slot) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
-    constexpr int H2 = C / 2;       // 16-B pieces per lane and row
-    constexpr int RW = 32 * C;      // dv2 per LDS row
+    constexpr int H2 = C / 2;       // 16-B pieces per lane, row and attribute
+    constexpr int RW = 32 * C * NA; // dv2 per LDS row
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;   // input from HBM
     constexpr bool kOut = ROLE == kRoleLast || ROLE == kRoleOnly;  // output to HBM
-    double uin[C];
+    double cur[NA][C];  // the row level q consumes
     if (kIn) {
 #pragma unroll
-        for (int h = 0; h < H2; ++h) {
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h) {
 #if MM_LOAD_COPY
-            uin[2 * h] = vcopy(st.raw[slot][h].x);
-            uin[2 * h + 1] = vcopy(st.raw[slot][h].y);
+                cur[a][2 * h] = vcopy(st.raw[slot][a][h].x);
+                cur[a][2 * h + 1] = vcopy(st.raw[slot][a][h].y);
 #else
-            uin[2 * h] = st.raw[slot][h].x;
-            uin[2 * h + 1] = st.raw[slot][h].y;
+                cur[a][2 * h] = st.raw[slot][a][h].x;
+                cur[a][2 * h + 1] = st.raw[slot][a][h].y;
 #endif
+            }
         }
         const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;
 #pragma unroll
-        for (int h = 0; h < H2; ++h) st.raw[slot][h] = load_row(x.in, o + 16 * h);
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h) st.raw[slot][a][h] = load_row(x.in[a], o + 16 * h);
+        }
     } else {
         const dv2* src = x.lds_in + ((i - G::B) % G::RL) * RW;  // i >= start >= D > B
 #pragma unroll
-        for (int h = 0; h < H2; ++h) {
-            const dv2 a = src[64 * h + x.lane];
-            uin[2 * h] = a.x;
-            uin[2 * h + 1] = a.y;
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h) {
+                const dv2 v = src[64 * (a * H2 + h) + x.lane];
+                cur[a][2 * h] = v.x;
+                cur[a][2 * h + 1] = v.y;
+            }
         }
     }
     if (!PRO) t = i - x.start;
-    double cur[C];  // MM_WIDE_ASC: the row level q consumes (level q-1's row of this iteration)
+    double uin[NA][C];  // descending order: level 0's input
 #pragma unroll
-    for (int k = 0; k < C; ++k) cur[k] = uin[k];
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+        for (int k = 0; k < C; ++k) uin[a][k] = cur[a][k];
+    }
 #pragma unroll
     for (int qq = 0; qq < KW; ++qq) {
         const int q = kSkew == 2 ? qq : KW - 1 - qq;
@@ -289,40 +415,57 @@ __device__ __forceinline__ void wave_iter(const WCtx<C>& x, WState<C, KW, U>& st
         if (PRO && m < 0) continue;  // compile time
         const int j = x.p * KW + q + 1;  // global level, 1-based
         const long long gx = x.g0 + (j - 1) + m;
-        double u[C];
+        double u[NA][C];
 #pragma unroll
-        for (int k = 0; k < C; ++k) u[k] = kSkew == 2 ? cur[k] : (q == 0 ? uin[k] : st.pend[q - 1][k]);
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int k = 0; k < C; ++k)
+                u[a][k] = kSkew == 2 ? cur[a][k] : (q == 0 ? uin[a][k] : st.pend[q - 1][a][k]);
+        }
         if (PRO && m < 2) {
-            wfill<C, BODY>(x.c, x.r, x.r8, gx, m, st.win[q], u);
+            lfill<C, NA, BODY>(x, gx, m, st.win[q], u);
             continue;
         }
-        double o[C];
-        wemit<C, BODY>(x.c, x.r, x.r8, gx, st.win[q], u, o);
+        double o[NA][C];
+        lemit<C, NA, BODY>(x, gx, st.win[q], u, o);
         if (RED) {
             const int r = x.rA - K + m + j - 2;  // output row of level j
-            accumc<C>(st.acc[q], r >= x.rA && r < x.rB, x.c, o);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.rA && r < x.rB, x.c, o[a]);
         }
         if (q == KW - 1) {
             if (kOut) {  // level K: output row m - 2 of the segment
                 const unsigned so = x.soff + (unsigned)(m - 2) * x.rowb;
 #pragma unroll
-                for (int h = 0; h < H2; ++h) store_row<NT>(x.out, so + 16 * h, o[2 * h], o[2 * h + 1]);
+                for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                    for (int h = 0; h < H2; ++h)
+                        store_row<NT>(x.out[a], so + 16 * h, o[a][2 * h], o[a][2 * h + 1]);
+                }
             } else {
                 dv2* dst = x.lds_out + (i % G::RL) * RW;
 #pragma unroll
-                for (int h = 0; h < H2; ++h) {
-                    dv2 a;
-                    a.x = o[2 * h];
-                    a.y = o[2 * h + 1];
-                    dst[64 * h + x.lane] = a;
+                for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                    for (int h = 0; h < H2; ++h) {
+                        dv2 v;
+                        v.x = o[a][2 * h];
+                        v.y = o[a][2 * h + 1];
+                        dst[64 * (a * H2 + h) + x.lane] = v;
+                    }
                 }
             }
-        } else if (kSkew == 2) {
-#pragma unroll
-            for (int k = 0; k < C; ++k) cur[k] = o[k];
         } else {
 #pragma unroll
-            for (int k = 0; k < C; ++k) st.pend[q][k] = o[k];
+            for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    if (kSkew == 2)
+                        cur[a][k] = o[a][k];
+                    else
+                        st.pend[q][a][k] = o[a][k];
+                }
+            }
         }
 #if MM_WIDE_LEVEL_BARRIER
         // at most MM_WIDE_LEVEL_BARRIER levels in flight: bounds the live registers
@@ -339,27 +482,30 @@ __device__ __forceinline__ void group_end(int i) {
 
 // Steady groups [b0, b1) (multiples of B) of one wave, B iterations per loop trip (ring
 // slot i mod U: U divides B).
-template <int C, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE>
-__device__ __forceinline__ void wave_groups(const WCtx<C>& x, WState<C, KW, U>& st, int b0,
-                                            int b1) {
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE>
+__device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st,
+                                            int b0, int b1) {
     for (int base = b0; base < b1; base += B) {
 #pragma unroll
         for (int tt = 0; tt < B; ++tt)
-            wave_iter<C, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, base + tt, 0, tt % U);
+            wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, base + tt, 0, tt % U);
         if (P > 1) wg_sync();
     }
 }
 
 // The whole schedule of one wave. MID: body of the groups whose rows are all interior.
-template <int C, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
-__device__ __forceinline__ void wave_run(const WCtx<C>& x, long long wid, int iend) {
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
+__device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, int iend) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     static_assert(B % U == 0, "ring slots repeat within a group");
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;
-    WState<C, KW, U> st;
+    WState<C, NA, KW, U> st;
 #pragma unroll
-    for (int q = 0; q < KW; ++q) st.acc[q] = 0.0;
+    for (int q = 0; q < KW; ++q) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) st.acc[q][a] = 0.0;
+    }
     int s;  // first iteration of the group loop
     if (kIn) {
         // start = 0: the prologue and the iterations up to the first group boundary are
@@ -367,15 +513,18 @@ __device__ __forceinline__ void wave_run(const WCtx<C>& x, long long wid, int ie
 #pragma unroll
         for (int k = 0; k < U; ++k) {
 #pragma unroll
-            for (int h = 0; h < C / 2; ++h)
-                st.raw[k][h] = load_row(x.in, x.voff + 16 * h + k * x.rowb);
+            for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                for (int h = 0; h < C / 2; ++h)
+                    st.raw[k][a][h] = load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
+            }
         }
 #pragma unroll
         for (int t = 0; t < G::T0; ++t) {
             if (t < G::S0)
-                wave_iter<C, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, t, t, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, t, t, t % U);
             else
-                wave_iter<C, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, t, 0, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, t, 0, t % U);
             if (P > 1 && (t + 1) % B == 0) wg_sync();
         }
         s = G::T0;
@@ -383,12 +532,12 @@ __device__ __forceinline__ void wave_run(const WCtx<C>& x, long long wid, int ie
         for (int i = 0; i < x.start; ++i) group_end<P, B>(i);
 #pragma unroll
         for (int t = 0; t < G::S0; ++t) {
-            wave_iter<C, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, x.start + t, t, 0);
+            wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, x.start + t, t, 0);
             group_end<P, B>(x.start + t);
         }
         s = x.start + G::S0;
         for (; s % B != 0; ++s) {
-            wave_iter<C, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, s, 0, 0);
+            wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, s, 0, 0);
             group_end<P, B>(s);
         }
     }
@@ -401,42 +550,47 @@ __device__ __forceinline__ void wave_run(const WCtx<C>& x, long long wid, int ie
     long long f1 = hi <= s ? s : s + (hi - s) / B * B;
     f0 = min(f0, (long long)iend);
     f1 = max(f0, min(f1, (long long)iend));
-    wave_groups<C, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
-    wave_groups<C, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
-    wave_groups<C, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
-    if (RED) {  // partials[partial_base + block][K]: this wave's KW levels
+    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
+    wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
+    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
+    if (RED) {  // partials[partial_base + block][K][NA]: this wave's KW levels
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
-            const double v = wave_sum_k(st.acc[q]);
-            if (x.lane == 0) x.partials[(x.pbase + wid) * K + x.p * KW + q] = v;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const double v = wave_sum_k(st.acc[q][a]);
+                if (x.lane == 0) x.partials[((x.pbase + wid) * K + x.p * KW + q) * NA + a] = v;
+            }
         }
     }
 }
 
-template <int C, int KW, int P, int U, int B, bool RED, int NT, int MID>
-__device__ __forceinline__ void wave_dispatch(const WCtx<C>& x, long long wid, int iend) {
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int MID>
+__device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, long long wid, int iend) {
     if (P == 1)
-        wave_run<C, KW, P, U, B, RED, NT, kRoleOnly, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleOnly, MID>(x, wid, iend);
     else if (x.p == 0)
-        wave_run<C, KW, P, U, B, RED, NT, kRoleFirst, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleFirst, MID>(x, wid, iend);
     else if (x.p == P - 1)
-        wave_run<C, KW, P, U, B, RED, NT, kRoleLast, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleLast, MID>(x, wid, iend);
     else
-        wave_run<C, KW, P, U, B, RED, NT, kRoleMid, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID>(x, wid, iend);
 }
 
-// K = KW * P fused steps per launch, one workgroup (P waves) per strip segment, C columns
-// per lane, MW waves per SIMD. The segment map is mm_passk.hpp's seg_map with blocks in
-// place of waves: the two edge strips first (A.th_edge rows), then the others (A.th rows).
-// RED: every level's sums of the block's output cells into partials[partial_base +
-// block][K]. NT & 1: non-temporal stores.
-template <int C, int KW, int P, int MW, int U, int B, bool RED, int NT>
+// K = KW * P fused steps per launch of an NA-attribute one-pass program (NA = 1: one
+// diffusion; NA > 1: pre-chain, diffusions of the attributes in diffuse_mask, post-chain),
+// one workgroup (P waves) per strip segment, C columns per lane, MW waves per SIMD. The
+// segment map is mm_passk.hpp's seg_map with blocks in place of waves: the two edge strips
+// first (A.th_edge rows), then the others (A.th rows). RED: every level's sums of the
+// block's output cells into partials[partial_base + block][K][NA]. NT & 1: non-temporal
+// stores.
+template <int C, int NA, int KW, int P, int MW, int U, int B, bool RED, int NT>
 __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     constexpr int LH = (K + C - 1) / C;  // halo lanes per side
     constexpr int OC = 64 * C - 2 * C * LH;  // output columns per strip
-    __shared__ dv2 lds[P > 1 ? P - 1 : 1][G::RL][32 * C];
+    __shared__ dv2 lds[P > 1 ? P - 1 : 1][G::RL][32 * C * NA];
     const int lane = threadIdx.x & 63;
     const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     long long blk = blockIdx.x;
@@ -456,7 +610,7 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
         rlo = A.rb0;
         rhi = A.rb1;
     }
-    WCtx<C> x;
+    WCtx<C, NA> x;
     int strip;
     seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, strip, x.rA, x.rB);
     const long long W = A.W;
@@ -480,15 +634,21 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     x.p = p;
     x.lane = lane;
     x.start = p * G::D;
+    x.dmask = A.diffuse_mask;
     x.g0 = A.x_init + x.rA - K;
-    x.r = A.drate[0];
-    x.r8 = x.r * 0.125;
-    x.in = rows_rsrc(A.in[0] + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K, A.pitch);
-    x.out = rows_rsrc(A.out[0] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        x.r[a] = A.drate[a];
+        x.r8[a] = x.r[a] * 0.125;
+        x.in[a] = rows_rsrc(A.in[a] + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K,
+                            A.pitch);
+        x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
+    }
     x.lds_in = p > 0 ? &lds[p - 1][0][0] : &lds[0][0][0];
     x.lds_out = p < P - 1 ? &lds[p][0][0] : &lds[0][0][0];
     x.partials = A.partials;
     x.pbase = A.partial_base;
+    x.A = &A;
 
     // every wave runs to iteration iend (a whole number of groups): the last wave emits
     // the segment's last row at iteration (P-1)*D + S0 + R - 1
@@ -498,12 +658,12 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     // it fixes up the lanes holding them
     const bool edge = !(c0 >= 1 && c0 + 64 * C <= W - 1);
     if (edge)
-        wave_dispatch<C, KW, P, U, B, RED, NT, kBodyEdge>(x, blk, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, blk, iend);
     else
-        wave_dispatch<C, KW, P, U, B, RED, NT, kBodyFast>(x, blk, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, blk, iend);
 }
 
-template <int C, int KW, int P, int MW, int NT>
+template <int C, int NA, int KW, int P, int MW, int NT>
 hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     constexpr int U = MM_WIDE_U;
     long long blocks = a.waves_total;
@@ -511,28 +671,28 @@ hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     const dim3 g((unsigned)blocks), b(64 * P);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
-        hipLaunchKernelGGL((mm_wide_kernel<C, KW, P, MW, U, MM_WIDE_B, true, NT>), g, b, 0, s, a);
+        hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, true, NT>), g, b, 0, s, a);
     else
-        hipLaunchKernelGGL((mm_wide_kernel<C, KW, P, MW, U, MM_WIDE_B, false, NT>), g, b, 0, s, a);
+        hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, false, NT>), g, b, 0, s, a);
     return hipGetLastError();
 }
 
 // a.seg must be set (segment schedule); variant bit 0: non-temporal stores.
-template <int C, int KW, int P, int MW>
+template <int C, int NA, int KW, int P, int MW>
 hipError_t wide_launch2(bool red, const PassArgs& a, hipStream_t s, int v) {
     if (!a.seg) return hipErrorInvalidValue;
-    return (v & 1) ? wide_launch3<C, KW, P, MW, 1>(red, a, s)
-                   : wide_launch3<C, KW, P, MW, 0>(red, a, s);
+    return (v & 1) ? wide_launch3<C, NA, KW, P, MW, 1>(red, a, s)
+                   : wide_launch3<C, NA, KW, P, MW, 0>(red, a, s);
 }
 
 // Resident workgroups per CU, from the kernel's registers (512 per SIMD lane, granules of
 // 8, at most 8 waves per SIMD) and its LDS (160 KiB per CU); see seg_blocks_per_cu_v.
-template <int C, int KW, int P, int MW, bool RED, int NT>
+template <int C, int NA, int KW, int P, int MW, bool RED, int NT>
 int wide_blocks_v() {
     hipFuncAttributes fa;
     const hipError_t e = hipFuncGetAttributes(
         &fa, reinterpret_cast<const void*>(
-                 mm_wide_kernel<C, KW, P, MW, MM_WIDE_U, MM_WIDE_B, RED, NT>));
+                 mm_wide_kernel<C, NA, KW, P, MW, MM_WIDE_U, MM_WIDE_B, RED, NT>));
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return 0;
@@ -544,11 +704,13 @@ int wide_blocks_v() {
     return std::max(blocks, 0);
 }
 
-template <int C, int KW, int P, int MW>
+template <int C, int NA, int KW, int P, int MW>
 int wide_blocks(bool red, int nt) {
     if (red)
-        return nt ? wide_blocks_v<C, KW, P, MW, true, 1>() : wide_blocks_v<C, KW, P, MW, true, 0>();
-    return nt ? wide_blocks_v<C, KW, P, MW, false, 1>() : wide_blocks_v<C, KW, P, MW, false, 0>();
+        return nt ? wide_blocks_v<C, NA, KW, P, MW, true, 1>()
+                  : wide_blocks_v<C, NA, KW, P, MW, true, 0>();
+    return nt ? wide_blocks_v<C, NA, KW, P, MW, false, 1>()
+              : wide_blocks_v<C, NA, KW, P, MW, false, 0>();
 }
 
 }  // namespace

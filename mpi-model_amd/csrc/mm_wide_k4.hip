@@ -5,9 +5,9 @@
 namespace mm {
 
 hipError_t wide_launch_k4(bool red, const PassArgs& a, hipStream_t s, int v) {
-    return wide_launch2<4, 1, 4, MM_WIDE_MIN_WAVES>(red, a, s, v);
+    return wide_launch2<4, 1, 1, 4, MM_WIDE_MIN_WAVES>(red, a, s, v);
 }
 
-int wide_blocks_k4(bool red, int nt) { return wide_blocks<4, 1, 4, MM_WIDE_MIN_WAVES>(red, nt); }
+int wide_blocks_k4(bool red, int nt) { return wide_blocks<4, 1, 1, 4, MM_WIDE_MIN_WAVES>(red, nt); }
 
 }  // namespace mm

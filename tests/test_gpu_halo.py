@@ -34,20 +34,20 @@ def make_chain(gpu, monkeypatch, H, W, G, n_attr=1, env=None):
 
 
 def run_chain(engines, steps, reduce_every=0):
-    """Advance every slab `steps` steps, halo_depth rows exchanged before every pass."""
+    """Advance every slab `steps` steps: before each pass of the engines' (common) plan,
+    that pass's depth of border rows is exchanged (mpimodel.run_host_halo's schedule)."""
     G = len(engines)
     depth = engines[0].info()["halo_depth"]
     assert all(e.info()["halo_depth"] == depth for e in engines)
-    done = 0
-    while done < steps:
-        k = min(depth, steps - done)
+    plan = engines[0].pass_plan(steps)
+    assert all(e.pass_plan(steps) == plan for e in engines)
+    for k in plan:
         halos = [e.halo_export(k) for e in engines]
         for g, e in enumerate(engines):
             e.halo_import(halos[g - 1][1] if g > 0 else None,
                           halos[g + 1][0] if g < G - 1 else None, nrows=k)
         for e in engines:
             e.run(k, reduce_every)
-        done += k
     return depth
 
 
@@ -134,8 +134,10 @@ C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
 
 @pytest.mark.parametrize("H,W,G", [(67, 300, 3), (40, 130, 8)])
 def test_deep_halo_chain_flow_program(gpu, O, monkeypatch, H, W, G):
-    # four attributes, chained transfers + four diffusions (config C5) on slabs
-    steps = 5
+    # four attributes, chained transfers + four diffusions (config C5) on slabs: passes of
+    # the level-split kernel (K = 8, 8, 4 on 22-row slabs; 4 on 5-row slabs), then a 1-step
+    # mm_passk_kernel pass
+    steps = 21
     na = 4
     engines = make_chain(gpu, monkeypatch, H, W, G, n_attr=na)
     try:
@@ -147,7 +149,8 @@ def test_deep_halo_chain_flow_program(gpu, O, monkeypatch, H, W, G):
                     e.add_diffuse(a, r)
                 else:
                     e.add_transfer(a, b, r)
-        assert engines[0].info()["halo_depth"] == 2
+        # the level-split kernel's K = 8 for four attributes, capped by the thinnest slab
+        assert engines[0].info()["halo_depth"] == min(8, H // G)
         run_chain(engines, steps, 1)
         got = [gather(engines, a) for a in range(na)]
         hists = [e.sums_history() for e in engines]

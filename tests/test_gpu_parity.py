@@ -196,11 +196,7 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}] + [
-    # the 8-column instances (ascending levels, no pend registers)
-    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": k} for k in (8, 12, 16)] + [
-    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
-    {"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": 16, "MM_XCD_REMAP": 1}]
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}]
 
 
 def env_id(env):
@@ -242,9 +238,7 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
                                  {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
                                  {"MM_STEPS_PER_PASS": 7},
                                  {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}]
-                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)]
-                         + [{"MM_WIDE": 1, "MM_WIDE_COLS": 8, "MM_STEPS_PER_PASS": k}
-                            for k in (8, 12, 16)],
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
                          ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
@@ -271,14 +265,13 @@ def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
 
 
 @pytest.mark.parametrize("k,wide", [(k, 0) for k in (2, 3, 4, 6, 7, 8, 9, 10)]
-                         + [(k, 1) for k in (4, 8, 12, 16, 20)] + [(k, 8) for k in (8, 12, 16)])
+                         + [(k, 1) for k in (4, 8, 12, 16, 20)])
 def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k, wide):
     # hipGraph replay of K-step passes with sums every 3rd step; 50 steps is not a
     # multiple of the graph length, so the tail runs eagerly (K >= 10: a graph holds
     # 6K steps -- an even number of flips and whole reduction periods -- so run 13K)
     H, W, steps = 300, 700, (50 if k < 10 else 13 * k)
-    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k, MM_WIDE=int(wide > 0),
-                        MM_WIDE_COLS=8 if wide == 8 else 4)
+    e = make_env_engine(gpu, monkeypatch, H, W, MM_STEPS_PER_PASS=k, MM_WIDE=wide)
     e.fill_random(0)
     e.add_diffuse(0, 0.2)
     e.run(steps, 3)
@@ -343,6 +336,65 @@ def test_flow_program_bit_exact(gpu, O, monkeypatch, env, flows, n_attr, shape):
         for a in range(n_attr):
             w = sums[k][a]
             assert abs(hist[k, a] - w) <= 1e-12 * abs(w), (k, a)
+
+
+# four-attribute one-pass programs on the level-split kernel (mm_wide_kernel, 2 columns per
+# lane, K = 8 / 4 passes): C5, and a pre-chain + two of four attributes diffusing + a post-
+# chain with a sink -- the non-diffusing attributes pass through every level
+WIDE_PROGRAMS = [
+    C5_FLOWS,
+    [(2, 0, 1, 0.1), (1, 0, 0, 0.1), (1, 2, 2, 0.2), (2, 3, 1, 0.05), (2, 2, -1, 0.01)],
+]
+
+
+@pytest.mark.parametrize("env", [{"MM_WIDE": 1}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4},
+                                 {"MM_WIDE": 1, "MM_SEG_WAVES": 0.01},
+                                 {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1}],
+                         ids=env_id)
+@pytest.mark.parametrize("prog", [0, 1])
+@pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9), (45, 700), (257, 512)])
+def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
+    H, W = shape
+    flows = WIDE_PROGRAMS[prog]
+    steps = 21  # 8 + 8 + 4 + 1 at K = 8
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    want, sums = O.program_step(fields, flows, steps=steps, sums_per_step=True)
+    e = make_env_engine(gpu, monkeypatch, H, W, n_attr=4, **env)
+    for a in range(4):
+        e.fill_random(a, seed=O.SEED + a)
+    add_flows(e, flows)
+    assert e.info()["kernel"] == 3
+    k = int(env.get("MM_STEPS_PER_PASS", 8))
+    plan = e.pass_plan(steps)
+    assert sum(plan) == steps and plan[0] == k
+    assert all(e.pass_kernel(p)[0] == (3 if p in (4, 8) else 2) for p in plan)
+    e.run(steps, reduce_every=1)
+    got = [e.download(a) for a in range(4)]
+    hist = e.sums_history()
+    e.close()
+    for a in range(4):
+        assert np.array_equal(got[a], want[a]), (a, int(np.count_nonzero(got[a] != want[a])))
+    assert hist.shape == (steps, 4)
+    for s_ in range(steps):
+        for a in range(4):
+            w = sums[s_][a]
+            assert abs(hist[s_, a] - w) <= 1e-12 * abs(w), (s_, a)
+
+
+def test_fill_after_freed_engine(gpu, O):
+    """A new engine's zeroing (hipMemset on the null stream) must be complete before its
+    fill runs on the engine's non-blocking stream: with memory another engine just freed
+    the fill used to be partly zeroed (found by a host-halo chain after C5 runs)."""
+    for rep in range(4):
+        with gpu.Engine(257, 512, n_attr=4) as big:
+            for a in range(4):
+                big.fill_random(a, seed=O.SEED + a)
+            big.add_diffuse(0, 0.1)
+            big.run(2, 1)
+        H, W = 64 + rep, 300
+        with gpu.Engine(H, W, 0, H // 2, rank=0, nranks=2, halo_mode=gpu.MM_HALO_HOST) as e:
+            e.fill_random(0)
+            assert np.array_equal(e.download(), O.fill_random(H, W)[:H // 2]), rep
 
 
 def test_large_grid_properties(gpu, O):

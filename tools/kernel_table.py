@@ -2,8 +2,7 @@
 """HIP-event time of one K-step pass per grid size and kernel (mm_passk_kernel at K, or
 mm_wide_kernel at K), the table the pass planner's cost model is fitted to.
 
-  python tools/kernel_table.py --sizes 32768x32768,16384x16384 --old 7,8,10 --wide 8,12,16,20 \
-      --wide8 8,12,16
+  python tools/kernel_table.py --sizes 32768x32768,16384x16384 --old 7,8,10 --wide 8,12,16,20
 """
 import argparse
 import json
@@ -17,9 +16,8 @@ import mpimodel as mm  # noqa: E402
 mm.lib()
 
 
-def one(H, W, k, wide, reps, cols=4):
-    env = {"MM_STEPS_PER_PASS": str(k), "MM_WIDE": "1" if wide else "0",
-           "MM_WIDE_COLS": str(cols)}
+def one(H, W, k, wide, reps):
+    env = {"MM_STEPS_PER_PASS": str(k), "MM_WIDE": "1" if wide else "0"}
     old = {key: os.environ.get(key) for key in env}
     os.environ.update(env)
     try:
@@ -51,7 +49,6 @@ def main():
     ap.add_argument("--sizes", default="32768x32768,16384x16384,8192x32768,4096x32768,4096x4096")
     ap.add_argument("--old", default="7,8,10")
     ap.add_argument("--wide", default="4,8,12,16,20")
-    ap.add_argument("--wide8", default="", help="K of the 8-column wide instances")
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     for sz in a.sizes.split(","):
@@ -60,8 +57,6 @@ def main():
             print(json.dumps(one(H, W, k, False, a.reps)), flush=True)
         for k in [int(x) for x in a.wide.split(",") if x]:
             print(json.dumps(one(H, W, k, True, a.reps)), flush=True)
-        for k in [int(x) for x in a.wide8.split(",") if x]:
-            print(json.dumps(one(H, W, k, True, a.reps, cols=8)), flush=True)
 
 
 if __name__ == "__main__":
