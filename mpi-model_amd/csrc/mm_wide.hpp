@@ -250,15 +250,16 @@ struct WState {
 };
 
 #ifndef MM_CHAIN_BRANCH
-#define MM_CHAIN_BRANCH 1  // transfer operands picked by scalar branches (0: chain_k's indexing)
+#define MM_CHAIN_BRANCH 0  // 1: transfer operands picked by scalar branches
 #endif
 
 // A transfer chain in declared order (oracle/mm_oracle.c, chain_k) on each of this lane's C
-// cells: out = r*u_a; u_a -= out; u_b += out (b < 0: the outflow leaves the system). a and
-// b are wave-uniform kernel arguments, so a scalar branch per transfer and operand picks
-// the attribute's registers: 3 fp64 operations per transfer and cell, where chain_k's
-// register-vector indexing (s_set_gpr_idx) adds two moves per operand access. The empty
-// asm keeps each case a branch (no speculation of the other attributes' cases into selects).
+// cells: out = r*u_a; u_a -= out; u_b += out (b < 0: the outflow leaves the system); a and
+// b are wave-uniform kernel arguments. Default: chain_k's 8-wide register vector indexed
+// with s_set_gpr_idx (two moves per operand access). MM_CHAIN_BRANCH picks the operands
+// with a scalar branch per transfer and operand instead (3 fp64 operations, no moves) --
+// 2.6x slower for C5 (profiles/r03/r3k: 51 vs 132 GCUPS at K = 4): the branches cut the
+// loop body into blocks the scheduler cannot interleave.
 template <int C, int NA>
 __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const signed char* ta,
                                            const signed char* tb, const double* tr) {

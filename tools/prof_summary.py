@@ -14,7 +14,7 @@ import os
 import statistics
 import sys
 
-KERNEL_RE = re.compile(r"mm_pass[2k]?_kernel")
+KERNEL_RE = re.compile(r"mm_(pass[2k]?|wide)_kernel")
 
 
 def rows(pattern):
