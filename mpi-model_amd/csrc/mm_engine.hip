@@ -76,6 +76,10 @@ struct FlowDesc {
     double rate;
 };
 
+// mm_wide_kernel block order: runs of kXcdChunk side-by-side strips per XCD (0: plain
+// round-robin); see wide_grid in mm_wide.hpp
+constexpr int kXcdChunk = 0;
+
 }  // namespace
 
 struct mm_engine {
@@ -109,6 +113,7 @@ struct mm_engine {
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
     double seg_edge = 0.0;   // edge-strip segment length / interior length (MM_SEG_EDGE; 0: auto)
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
+    int xcd_chunk = kXcdChunk;  // mm_wide_kernel: runs of this many strips per XCD (MM_XCD_CHUNK, 0: off)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
     int bpc[2][2][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt][k]
@@ -529,7 +534,7 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     mm::PassArgs A;
     fill_args(e, e->passes[0], A);
     A.nstrips = (int)nstrips_wide(e, k);
-    A.xcd_remap = e->xcd;
+    A.xcd_remap = e->xcd ? e->xcd : e->xcd_chunk;  // MM_XCD_REMAP=1, else XCD chunks
     long long total_blocks = 0;
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(split_begin(e, depth));
@@ -629,7 +634,7 @@ bool passk_ok(const mm_engine* e) {
     return true;
 }
 
-constexpr int kWideAuto = 16;      // auto steps per pass of the wide kernel, one attribute
+constexpr int kWideAuto = 20;      // auto steps per pass of the wide kernel, one attribute
 constexpr int kWideAutoMulti = 8;  // several attributes
 
 // Steps per K-step pass: the configured K, capped so that a depth-K halo never reaches
@@ -687,18 +692,19 @@ bool pass_len_ok(const mm_engine* e, long long k) {
     return k >= 1 && (k <= mm::passk_max_steps(e->na) || use_wide(e, (int)k));
 }
 
-// Modelled time of one k-step pass on a large slab with the wide kernel on (HIP-event pass
-// times at 32768^2, profiles/r03/kernel_table: mm_passk_kernel K <= 7 stream-bound at
-// ~3.5 ms, K = 8 / 9 / 10 at 3.66 / 4.14 / 4.62 ms; mm_wide_kernel K = 4 / 8 / 12 / 16 / 20
-// at 3.69 / 3.68 / 4.90 / 6.22 / 8.13 ms), in ms.
+// Modelled time of one k-step pass on a large slab with the wide kernel on, in ms at
+// 32768^2: mm_passk_kernel K <= 7 stream-bound at ~3.5 ms, K = 8 / 9 / 10 at 3.66 / 4.14 /
+// 4.62 (profiles/r02b); mm_wide_kernel K = 4 / 8 at 3.69 / 3.68 (profiles/r03/kernel_table)
+// and K = 12 / 16 / 20 at 0.778 / 1 / 1.236 of the K = 16 pass (one box,
+// profiles/r03/xcd2/kernel_table.log: 5120 / 6578 / 8128 us; K = 20 with ascending levels).
 double wide_plan_cost(const mm_engine* e, int k) {
     if (use_wide(e, k)) {
         switch (k) {
             case 4: return 3.69;
             case 8: return 3.68;
-            case 12: return 4.90;
+            case 12: return 4.84;
             case 16: return 6.22;
-            default: return 8.13;
+            default: return 7.69;
         }
     }
     if (k <= 7) return 3.50;
@@ -707,7 +713,7 @@ double wide_plan_cost(const mm_engine* e, int k) {
 
 // Steps of the first pass of the cheapest plan of n steps (wide on, K auto): a dynamic
 // program over the pass lengths both kernels have (capped by the chain's thinnest slab).
-// Runs longer than kDpMax steps start with a pass of the best per-step length (K = 16).
+// Runs longer than kDpMax steps start with a pass of the best per-step length (K = 20).
 int wide_plan_first(const mm_engine* e, long long n, int kcap) {
     constexpr int kDpMax = 256;
     if (n > kDpMax) return std::min(kWideAuto, kcap);
@@ -1034,6 +1040,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
+    if (const char* c = std::getenv("MM_XCD_CHUNK")) e->xcd_chunk = std::max(0, std::atoi(c)) == 1 ? 2 : std::max(0, std::atoi(c));
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
         if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4, 1) || mm::wide_has(v, 2, 4)))))

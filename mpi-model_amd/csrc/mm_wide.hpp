@@ -578,6 +578,25 @@ __device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, long long wi
         wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID>(x, wid, iend);
 }
 
+// Edge-strip blocks of range a (seg_map puts them first), rounded up to a multiple of 8.
+__host__ __device__ inline long long wide_edge_blocks8(const PassArgs& A) {
+    const long long n = A.ra1 - A.ra0;
+    const long long e = A.nstrips < 3 || n <= 0 ? 0 : 2 * ((n + A.th_edge - 1) / A.th_edge);
+    return (e + 7) / 8 * 8;
+}
+
+// Grid of a launch: waves_total blocks, padded for the XCD orders (the padding blocks
+// map past waves_total and exit at once).
+__host__ __device__ inline long long wide_grid(const PassArgs& A) {
+    const long long t = A.waves_total;
+    if (A.xcd_remap == 1) return (t + 7) / 8 * 8;
+    if (A.xcd_remap > 1) {
+        const long long e8 = wide_edge_blocks8(A), q = 8LL * A.xcd_remap;
+        return t <= e8 ? e8 : e8 + (t - e8 + q - 1) / q * q;
+    }
+    return t;
+}
+
 // K = KW * P fused steps per launch of an NA-attribute one-pass program (NA = 1: one
 // diffusion; NA > 1: pre-chain, diffusions of the attributes in diffuse_mask, post-chain),
 // one workgroup (P waves) per strip segment, C columns per lane, MW waves per SIMD. The
@@ -595,9 +614,20 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     const int lane = threadIdx.x & 63;
     const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     long long blk = blockIdx.x;
-    if (A.xcd_remap) {
+    if (A.xcd_remap == 1) {
         const long long per = gridDim.x / 8;
         blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    } else if (A.xcd_remap > 1) {
+        // XCD chunks (wide_grid): hardware block b runs on XCD b % 8. The first e8 blocks
+        // (the two edge strips' segments, rounded up to 8) keep that round-robin order, so
+        // the slow edge blocks spread over all XCDs; after them each XCD takes runs of
+        // S = xcd_remap consecutive logical blocks -- side-by-side strips of one row
+        // segment, whose 2K overlapping columns its L2 then serves once
+        const long long e8 = wide_edge_blocks8(A);
+        if (blk >= e8) {
+            const long long S = A.xcd_remap, r = blk - e8, j = r / 8;
+            blk = e8 + (j / S) * 8 * S + (r % 8) * S + j % S;
+        }
     }
     if (blk >= A.waves_total) return;  // the whole block: no barrier is left waiting
 
@@ -667,8 +697,7 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
 template <int C, int NA, int KW, int P, int MW, int NT>
 hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     constexpr int U = MM_WIDE_U;
-    long long blocks = a.waves_total;
-    if (a.xcd_remap) blocks = (blocks + 7) / 8 * 8;
+    const long long blocks = wide_grid(a);
     const dim3 g((unsigned)blocks), b(64 * P);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)

@@ -1,5 +1,14 @@
 // mm_wide_k20.hip -- instances of the level-split K-step kernel (mm_wide.hpp) for K = 20:
 // 5 level(s) per wave, 4 waves per workgroup.
+// Tuning (tools/libsweep.py, profiles/r03/var_k20): levels in ascending order (no pend
+// registers: VGPR spills 504 -> 27) and 2 input rows prefetched -- 7 % faster at 32768^2
+// than the pend hand-off with 4 rows (8260 vs 8891 us per 20-step pass on one box).
+#ifndef MM_WIDE_ASC
+#define MM_WIDE_ASC 1
+#endif
+#ifndef MM_WIDE_U
+#define MM_WIDE_U 2
+#endif
 #include "mm_wide.hpp"
 
 namespace mm {

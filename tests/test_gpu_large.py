@@ -82,7 +82,7 @@ WIDE_K = (4, 8, 12, 16, 20)
 def test_pass_planner_plans(gpu, monkeypatch):
     """mm_pass_plan. Slabs of >= 2^28 cells run the level-split kernel: the planner's
     cheapest plan over both kernels' lengths -- one K = 20 pass for the driver's 20 steps,
-    K = 16 passes for long runs. MM_PASS_PLAN=0: passes of K = 16 and a tail.
+    K = 20 passes for long runs. MM_PASS_PLAN=0: passes of K = 20 and a tail.
     MM_WIDE=0 (round 2): 10 + 10 on 8192 x 32768, K = 8 for long runs. Smaller slabs
     (4096^2) keep mm_passk_kernel's balanced passes of K = 7."""
     for H, W in ((8192, 32768), (16384, 16384)):
@@ -95,13 +95,14 @@ def test_pass_planner_plans(gpu, monkeypatch):
             assert e.pass_plan(9) == [9]
             assert e.pass_plan(0) == []
             p = e.pass_plan(1000)
-            assert sum(p) == 1000 and len(p) <= 63
+            assert sum(p) == 1000 and len(p) <= 51
             assert all(k in WIDE_K or k <= 10 for k in p)
-            assert p.count(16) >= 55
+            assert p.count(20) >= 45
     monkeypatch.setenv("MM_PASS_PLAN", "0")
     with gpu.Engine(8192, 32768) as e:
         e.add_diffuse(0, RATE)
-        assert e.pass_plan(20) == [16, 4]
+        assert e.pass_plan(20) == [20]
+        assert e.pass_plan(45) == [20, 20, 5]
     monkeypatch.delenv("MM_PASS_PLAN")
     monkeypatch.setenv("MM_WIDE", "0")
     with gpu.Engine(8192, 32768) as e:
