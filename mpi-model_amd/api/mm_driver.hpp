@@ -21,8 +21,8 @@
 //     owns, so the scalar halo messages src/Model.hpp:202-204 / :228-230 disappear;
 //   * a whole-grid flow (Exponencial(rate)) runs step_count(time, time_step) steps
 //     (the commented-out loop, src/Model.hpp:180-183) with border rows exchanged over
-//     RCCL (workers on distinct GPUs) or through MPI (workers sharing a GPU: halo_depth
-//     rows per exchange, then halo_depth steps on the device);
+//     RCCL (workers on distinct GPUs) or through MPI (workers sharing a GPU: before each
+//     K-step pass of the engine's plan, K rows per exchange);
 //   * the per-rank text dump and the master's merge keep the reference's format
 //     (src/Model.hpp:97-131,245-260).
 // Environment: MM_OUTPUT_DIR (default "../output", as the reference),
@@ -256,16 +256,16 @@ double worker(const WorkerComm& w, int rank, int P, const FlowSpec& f, int owner
         MPI_Barrier(w.wcomm);
         const auto t0 = std::chrono::steady_clock::now();
         if (d.halo_mode == MM_HALO_HOST) {
-            // workers sharing a GPU: halo_depth rows per MPI exchange, then as many steps
-            // in one K-step kernel pass
-            const int depth = e.info().halo_depth;
+            // workers sharing a GPU: before each K-step pass of the engine's plan (the same
+            // on every worker: it is sized by the thinnest slab) that pass's K border rows
+            // go through MPI, then the pass runs
+            const std::vector<int> plan = e.pass_plan(n);
+            const int depth = plan.empty() ? 1 : *std::max_element(plan.begin(), plan.end());
             const size_t sz = (size_t)depth * (size_t)W;
             std::vector<double> top(sz), bot(sz), gtop(sz), gbot(sz);
-            for (long long s = 0; s < n;) {
-                const int k = (int)std::min<long long>(depth, n - s);
+            for (const int k : plan) {
                 host_halo(e, w, k, top, bot, gtop, gbot);
                 e.run(k, 1);
-                s += k;
             }
         } else {
             e.run(n, 1);

@@ -40,6 +40,14 @@ public:
         return applied != 0;
     }
     void run(long long steps, long long reduce_every) { check(mm_run(e_, steps, reduce_every)); }
+    // the K-step passes a run of `steps` steps launches (the engine's pass planner)
+    std::vector<int> pass_plan(long long steps) {
+        int n = 0;
+        check(mm_pass_plan(e_, steps, nullptr, 0, &n));
+        std::vector<int> lens((size_t)n);
+        if (n) check(mm_pass_plan(e_, steps, lens.data(), n, &n));
+        return lens;
+    }
     void synchronize() { check(mm_synchronize(e_)); }
     std::vector<double> sums() {
         std::vector<double> s(d_.n_attr);
