@@ -19,7 +19,7 @@ def main():
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             rows.extend(csv.DictReader(fh))
-    rows = [r for r in rows if "mm_pass" in r.get("Kernel_Name", "")]
+    rows = [r for r in rows if "mm_pass" in r.get("Kernel_Name", "") or "mm_wide" in r.get("Kernel_Name", "")]
     if not rows:
         sys.exit("no step-kernel dispatches")
     by_kernel = {}
