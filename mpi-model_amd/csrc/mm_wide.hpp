@@ -92,6 +92,21 @@ namespace {
 // registers per level fewer, the scheduler interleaves consecutive iterations instead).
 constexpr int kSkew = MM_WIDE_ASC ? 2 : 3;
 
+#ifndef MM_WIDE_XPOSE
+#define MM_WIDE_XPOSE 1  // C = 8: rows in / out of HBM coalesced, transposed through LDS
+#endif
+
+// With 8 columns per lane a lane's slice of a row is 64 B: loaded / stored in place, each
+// 16-B wave-instruction touches 64 separate 64-B segments and the texture addresser
+// becomes the bottleneck (profiles/r03/w8probe: 2.9x its busy cycles for the same bytes).
+// XPOSE moves rows piece-major instead -- piece h of lane l = columns c0 + 128h + 2l, +1,
+// 1 KiB contiguous per instruction -- and transposes them through a 4-KiB LDS scratch of
+// the first (input) and the last (output) wave.
+template <int C>
+struct WXpose {
+    static constexpr bool on = C == 8 && MM_WIDE_XPOSE;
+};
+
 enum { kBodyFast = 0, kBodyEdge = 1, kBodyGen = 2 };
 
 // What every level of a wave needs besides its windows.
@@ -233,6 +248,8 @@ struct WCtx {
     long long g0;         // global row of input row 0 (rA - K)
     double r[NA], r8[NA];
     unsigned voff, soff, rowb;
+    unsigned xvoff[C / 2], xsoff[C / 2];  // WXpose: per-piece load / store offsets
+    dv2* lds_x;                           // WXpose: this wave's transpose scratch
     __amdgpu_buffer_rsrc_t in[NA], out[NA];
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
@@ -370,7 +387,22 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;   // input from HBM
     constexpr bool kOut = ROLE == kRoleLast || ROLE == kRoleOnly;  // output to HBM
     double cur[NA][C];  // the row level q consumes
-    if (kIn) {
+    if constexpr (kIn && WXpose<C>::on) {
+        // the prefetched row is piece-major: through the scratch into this lane's columns
+        static_assert(NA == 1, "one attribute");
+#pragma unroll
+        for (int h = 0; h < H2; ++h) x.lds_x[64 * h + x.lane] = st.raw[slot][0][h];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int h = 0; h < H2; ++h) {
+            const dv2 v = x.lds_x[H2 * x.lane + h];
+            cur[0][2 * h] = v.x;
+            cur[0][2 * h + 1] = v.y;
+        }
+        const unsigned ro = (unsigned)(i + U) * x.rowb;
+#pragma unroll
+        for (int h = 0; h < H2; ++h) st.raw[slot][0][h] = load_row(x.in[0], x.xvoff[h] + ro);
+    } else if (kIn) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
@@ -435,7 +467,22 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
             for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.rA && r < x.rB, x.c, o[a]);
         }
         if (q == KW - 1) {
-            if (kOut) {  // level K: output row m - 2 of the segment
+            if constexpr (kOut && WXpose<C>::on) {  // level K: output row m - 2, piece-major
+                const unsigned ro = (unsigned)(m - 2) * x.rowb;
+#pragma unroll
+                for (int h = 0; h < H2; ++h) {
+                    dv2 v;
+                    v.x = o[0][2 * h];
+                    v.y = o[0][2 * h + 1];
+                    x.lds_x[H2 * x.lane + h] = v;
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int h = 0; h < H2; ++h) {
+                    const dv2 v = x.lds_x[64 * h + x.lane];
+                    store_row<NT>(x.out[0], x.xsoff[h] + ro, v.x, v.y);
+                }
+            } else if (kOut) {  // level K: output row m - 2 of the segment
                 const unsigned so = x.soff + (unsigned)(m - 2) * x.rowb;
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
@@ -517,7 +564,9 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
             for (int a = 0; a < NA; ++a) {
 #pragma unroll
                 for (int h = 0; h < C / 2; ++h)
-                    st.raw[k][a][h] = load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
+                    st.raw[k][a][h] = WXpose<C>::on
+                                          ? load_row(x.in[a], x.xvoff[h] + k * x.rowb)
+                                          : load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
             }
         }
 #pragma unroll
@@ -611,6 +660,7 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     constexpr int LH = (K + C - 1) / C;  // halo lanes per side
     constexpr int OC = 64 * C - 2 * C * LH;  // output columns per strip
     __shared__ dv2 lds[P > 1 ? P - 1 : 1][G::RL][32 * C * NA];
+    __shared__ dv2 lds_x[WXpose<C>::on ? 2 : 1][WXpose<C>::on ? 32 * C : 1];
     const int lane = threadIdx.x & 63;
     const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     long long blk = blockIdx.x;
@@ -652,6 +702,16 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     x.voff = in_row ? (unsigned)(y0 * 8) : kOOBk;
     // columns past W inside the pitch are padding: writing them is harmless
     x.soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
+    if (WXpose<C>::on) {  // piece h of lane l: columns c0 + 128h + 2l, +1
+#pragma unroll
+        for (int h = 0; h < C / 2; ++h) {
+            const long long yc = c0 + 128LL * h + 2 * lane;
+            x.xvoff[h] = yc >= 0 && yc < A.pitch ? (unsigned)(yc * 8) : kOOBk;
+            const bool st_ok = yc >= c0 + C * LH && yc < c0 + 64 * C - C * LH && yc < W;
+            x.xsoff[h] = st_ok ? (unsigned)(yc * 8) : kOOBk;
+        }
+        x.lds_x = &lds_x[p == 0 ? 0 : (WXpose<C>::on ? 1 : 0)][0];
+    }
     x.rowb = (unsigned)(A.pitch * 8);
     x.c.H = A.H;
     x.c.special = false;

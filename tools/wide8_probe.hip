@@ -9,10 +9,13 @@
 #include <vector>
 
 #ifndef MM_WIDE_U
-#define MM_WIDE_U 4
+#define MM_WIDE_U 2
 #endif
 #ifndef MM_WIDE_B
-#define MM_WIDE_B 4
+#define MM_WIDE_B 2
+#endif
+#ifndef MM_WIDE_ASC
+#define MM_WIDE_ASC 1
 #endif
 #include "mm_wide.hpp"
 
@@ -27,9 +30,9 @@ using namespace mm;
         }                                                                     \
     } while (0)
 
-template <int C, int MW>
+template <int C, int KW, int MW>
 double run(double* in, double* out, long long H, long long W, long long pitch, int reps) {
-    constexpr int KW = 2, P = 4, K = KW * P;
+    constexpr int P = 4, K = KW * P;
     constexpr int LH = (K + C - 1) / C, OC = 64 * C - 2 * C * LH;
     PassArgs A;
     std::memset(&A, 0, sizeof A);
@@ -42,7 +45,7 @@ double run(double* in, double* out, long long H, long long W, long long pitch, i
     A.diffuse_mask = 1;
     A.seg = 1;
     A.nstrips = (int)((W + OC - 1) / OC);
-    const int blocks_per_cu = wide_blocks<C, 1, KW, P, MW>(false, 1);
+    const int blocks_per_cu = wide_blocks_v<C, 1, KW, P, MW, false, 1>();
     // segments: ~4 resident block waves, edge strips at half length
     const long long want = 4LL * 256 * std::max(1, blocks_per_cu);
     const double units = (A.nstrips - 2) + 2.0 / 0.5;
@@ -56,10 +59,10 @@ double run(double* in, double* out, long long H, long long W, long long pitch, i
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    CHECK((wide_launch2<C, 1, KW, P, MW>(false, A, 0, 1)));  // warm
+    CHECK((wide_launch3<C, 1, KW, P, MW, 1>(false, A, 0)));  // warm
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventRecord(a, 0));
-    for (int i = 0; i < reps; ++i) CHECK((wide_launch2<C, 1, KW, P, MW>(false, A, 0, 1)));
+    for (int i = 0; i < reps; ++i) CHECK((wide_launch3<C, 1, KW, P, MW, 1>(false, A, 0)));
     CHECK(hipEventRecord(b, 0));
     CHECK(hipEventSynchronize(b));
     float ms = 0;
@@ -86,8 +89,9 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     double* in = b0 + ghost * pitch;
     double* out = b1 + ghost * pitch;
-    if (which == 0 || which == 4) run<4, 2>(in, out, H, W, pitch, reps);
-    if (which == 0 || which == 8) run<8, 2>(in, out, H, W, pitch, reps);
+    if (which == 0 || which == 4) run<4, 2, 2>(in, out, H, W, pitch, reps);
+    if (which == 0 || which == 8) run<8, 2, 2>(in, out, H, W, pitch, reps);
+    if (which == 0 || which == 12) run<8, 3, 2>(in, out, H, W, pitch, reps);
     CHECK(hipFree(b0));
     CHECK(hipFree(b1));
     return 0;
