@@ -116,7 +116,7 @@ struct mm_engine {
     int xcd_chunk = kXcdChunk;  // mm_wide_kernel: runs of this many strips per XCD (MM_XCD_CHUNK, 0: off)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
-    int bpc[2][2][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt][k]
+    int bpc[2][4][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt | ring][k]
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -246,6 +246,18 @@ hipEvent_t next_event(mm_engine* e) {
 // Columns per lane of the wide kernel: 4 for one attribute, 2 for several.
 int wcols(const mm_engine* e, int) { return e->na > 1 ? 2 : 4; }
 
+// Variant bit 1 of a wide launch: a one-pass program of four attributes whose pre-chain
+// is the ring of transfers t -> t+1 mod 4 in that order, without a post-chain (config C5's
+// topology), runs the instance with the chain's operands fixed at compile time.
+int wring(const mm_engine* e) {
+    if (e->na != 4 || e->passes.size() != 1) return 0;
+    const Pass& p = e->passes[0];
+    if ((int)p.pre.size() != e->na || !p.post.empty()) return 0;
+    for (int t = 0; t < e->na; ++t)
+        if (p.pre[t].a != t || p.pre[t].b != (t + 1) % e->na) return 0;
+    return 2;
+}
+
 // Launch a one-step pass (kpass == 0), a K-step pass (kpass = K > 0: mm_passk_kernel;
 // kpass = -K: mm_wide_kernel) covering `rows`
 // rows on the compute stream, with an event pair around it when timing. Algorithmic
@@ -264,7 +276,7 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
     if (kpass > 0)
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else if (kpass < 0)
-        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp, e->variant));
+        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp, e->variant | wring(e)));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -487,7 +499,7 @@ long long nstrips_wide(const mm_engine* e, int k) {
 // iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
 // profiles/r03/kernel_table).
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
-    const int nt = e->variant & 1;
+    const int nt = (e->variant & 1) | wring(e);
     const int c = wcols(e, k);
     int& bpc = e->bpc[red ? 1 : 0][nt][k];
     if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, e->na, red, nt));
@@ -550,7 +562,7 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
         B.waves_total = 2 * B.waves_a;
         B.partial_base = interior;
-        MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, 0));
+        MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, wring(e)));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
@@ -1193,7 +1205,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na);
         info->kernel = 3;
         info->seg_waves_per_cu =
-            e->bpc[0][e->variant & 1][spl] * mm::wide_waves_per_block(spl, c, e->na);
+            e->bpc[0][(e->variant & 1) | wring(e)][spl] * mm::wide_waves_per_block(spl, c, e->na);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);

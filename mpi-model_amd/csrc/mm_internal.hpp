@@ -66,7 +66,9 @@ int passk_waves_per_cu(int k, int na, bool red, int nt);
 // {4, 8}. One workgroup of wide_waves_per_block(k, c, na) waves per strip segment, segment
 // schedule only (a.seg; a.th / a.th_edge rows per block, a.waves_a / a.waves_total count
 // BLOCKS), a.nstrips = ceil(W / wide_out_cols(k, c)). red: every level's sums into
-// partials[block][k][na]. variant bit 0: non-temporal stores.
+// partials[block][k][na]. variant (and nt) bit 0: non-temporal stores; bit 1: four
+// attributes whose pre-chain is the ring t -> t+1 mod 4 and no post-chain (K = 8: the
+// compile-time-chain instance).
 bool wide_has(int k, int c, int na);
 int wide_out_cols(int k, int c);
 int wide_waves_per_block(int k, int c, int na);

@@ -105,6 +105,8 @@ int wide_waves_per_block(int k, int c, int na) {
 
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt) {
     if (!wide_has(k, c, na)) return 0;
+    if (na > 1 && k == 8 && (nt & 2)) return widear_blocks_k8(na, red, nt & 1);
+    nt &= 1;
     if (na > 1) return k == 4 ? widea_blocks_k4(na, red, nt) : widea_blocks_k8(na, red, nt);
     switch (k) {
         case 4: return wide_blocks_k4(red, nt);
@@ -119,6 +121,7 @@ hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStr
                        int variant) {
     if (a.waves_total <= 0) return hipSuccess;
     if (!wide_has(k, c, na)) return hipErrorInvalidValue;
+    if (na > 1 && k == 8 && (variant & 2)) return widear_launch_k8(na, red, a, s, variant & 1);
     if (na > 1)
         return k == 4 ? widea_launch_k4(na, red, a, s, variant)
                       : widea_launch_k8(na, red, a, s, variant);

@@ -67,6 +67,9 @@ MM_WIDE_DECL(20)
 MM_WIDEA_DECL(4)
 MM_WIDEA_DECL(8)
 #undef MM_WIDEA_DECL
+// four attributes whose pre-chain is the ring t -> t+1 mod 4 (mm_widear_k*.hip)
+hipError_t widear_launch_k8(int na, bool red, const PassArgs& a, hipStream_t s, int v);
+int widear_blocks_k8(int na, bool red, int nt);
 
 namespace {
 
@@ -104,7 +107,7 @@ constexpr int kSkew = MM_WIDE_ASC ? 2 : 3;
 // the first (input) and the last (output) wave.
 template <int C>
 struct WXpose {
-    static constexpr bool on = C == 8 && MM_WIDE_XPOSE;
+    static constexpr bool on = C >= 6 && MM_WIDE_XPOSE;
 };
 
 enum { kBodyFast = 0, kBodyEdge = 1, kBodyGen = 2 };
@@ -277,10 +280,30 @@ struct WState {
 // with a scalar branch per transfer and operand instead (3 fp64 operations, no moves) --
 // 2.6x slower for C5 (profiles/r03/r3k: 51 vs 132 GCUPS at K = 4): the branches cut the
 // loop body into blocks the scheduler cannot interleave.
+#ifndef MM_CHAIN_RING
+#define MM_CHAIN_RING 0  // 1: pre-chains are the ring a = t, b = t+1 mod NA (engine-checked)
+#endif
+
 template <int C, int NA>
 __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const signed char* ta,
                                            const signed char* tb, const double* tr) {
-#if MM_CHAIN_BRANCH
+#if MM_CHAIN_RING
+    // the ring of transfers t -> t+1 mod NA (C5's chain): compile-time operands, 3 fp64
+    // operations per transfer and cell (the engine sends only such chains here)
+    (void)n;
+    (void)ta;
+    (void)tb;
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+        const double r = tr[t];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const double out = r * u[t][k];
+            u[t][k] = u[t][k] - out;
+            u[(t + 1) % NA][k] = u[(t + 1) % NA][k] + out;
+        }
+    }
+#elif MM_CHAIN_BRANCH
 #pragma unroll
     for (int t = 0; t < kMaxChain; ++t) {
         if (t >= n) break;  // wave-uniform
@@ -367,7 +390,7 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
             wemit<C, BODY>(x.c, x.r[a], x.r8[a], gx, w[a], u[a], o[a]);
         }
     }
-    if (NA > 1 && x.A->npost)
+    if (NA > 1 && !MM_CHAIN_RING && x.A->npost)
         chain_cols<C, NA>(o, x.A->npost, x.A->post_a, x.A->post_b, x.A->post_r);
 }
 

@@ -1,0 +1,25 @@
+// mm_widear_k8.hip -- the four-attribute level-split K-step kernel (mm_widea_k8.hip) for
+// programs whose pre-chain is the ring of transfers t -> t+1 mod 4 and that have no
+// post-chain (config C5's topology): the chain's operands are compile-time registers
+// instead of an indexed register vector. The engine checks the pattern (is_ring).
+#ifndef MM_WIDE_U
+#define MM_WIDE_U 2
+#endif
+#ifndef MM_WIDE_B
+#define MM_WIDE_B 2
+#endif
+#define MM_CHAIN_RING 1
+#include "mm_wide.hpp"
+
+namespace mm {
+
+hipError_t widear_launch_k8(int na, bool red, const PassArgs& a, hipStream_t s, int v) {
+    if (na == 4) return wide_launch2<2, 4, 1, 8, 2>(red, a, s, v);
+    return hipErrorInvalidValue;
+}
+
+int widear_blocks_k8(int na, bool red, int nt) {
+    return na == 4 ? wide_blocks<2, 4, 1, 8, 2>(red, nt) : 0;
+}
+
+}  // namespace mm

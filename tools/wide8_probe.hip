@@ -30,7 +30,7 @@ using namespace mm;
         }                                                                     \
     } while (0)
 
-template <int C, int KW, int MW>
+template <int C, int KW, int MW, int GB = MM_WIDE_B>
 double run(double* in, double* out, long long H, long long W, long long pitch, int reps) {
     constexpr int P = 4, K = KW * P;
     constexpr int LH = (K + C - 1) / C, OC = 64 * C - 2 * C * LH;
@@ -45,7 +45,14 @@ double run(double* in, double* out, long long H, long long W, long long pitch, i
     A.diffuse_mask = 1;
     A.seg = 1;
     A.nstrips = (int)((W + OC - 1) / OC);
-    const int blocks_per_cu = wide_blocks_v<C, 1, KW, P, MW, false, 1>();
+    const int blocks_per_cu = [] {
+        hipFuncAttributes fa;
+        CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
+            mm_wide_kernel<C, 1, KW, P, MW, MM_WIDE_U, GB, false, 1>)));
+        const int regs = (fa.numRegs + 7) / 8 * 8;
+        int b = std::min(8, 512 / regs) * 4 / P;
+        return std::min(b, (int)(160 * 1024 / fa.sharedSizeBytes));
+    }();
     // segments: ~4 resident block waves, edge strips at half length
     const long long want = 4LL * 256 * std::max(1, blocks_per_cu);
     const double units = (A.nstrips - 2) + 2.0 / 0.5;
@@ -59,17 +66,22 @@ double run(double* in, double* out, long long H, long long W, long long pitch, i
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    CHECK((wide_launch3<C, 1, KW, P, MW, 1>(false, A, 0)));  // warm
+    auto launch = [&] {
+        hipLaunchKernelGGL((mm_wide_kernel<C, 1, KW, P, MW, MM_WIDE_U, GB, false, 1>),
+                           dim3((unsigned)A.waves_total), dim3(64 * P), 0, 0, A);
+        return hipGetLastError();
+    };
+    CHECK(launch());  // warm
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventRecord(a, 0));
-    for (int i = 0; i < reps; ++i) CHECK((wide_launch3<C, 1, KW, P, MW, 1>(false, A, 0)));
+    for (int i = 0; i < reps; ++i) CHECK(launch());
     CHECK(hipEventRecord(b, 0));
     CHECK(hipEventSynchronize(b));
     float ms = 0;
     CHECK(hipEventElapsedTime(&ms, a, b));
-    std::printf("{\"cols\": %d, \"K\": %d, \"strips\": %d, \"rows_per_block\": %lld, \"blocks\": %lld, "
+    std::printf("{\"B\": %d, \"cols\": %d, \"K\": %d, \"strips\": %d, \"rows_per_block\": %lld, \"blocks\": %lld, "
                 "\"blocks_per_cu\": %d, \"pass_us\": %.1f}\n",
-                C, K, A.nstrips, r, (long long)A.waves_total, blocks_per_cu, 1e3 * ms / reps);
+                GB, C, K, A.nstrips, r, (long long)A.waves_total, blocks_per_cu, 1e3 * ms / reps);
     return ms / reps;
 }
 
@@ -89,9 +101,12 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     double* in = b0 + ghost * pitch;
     double* out = b1 + ghost * pitch;
-    if (which == 0 || which == 4) run<4, 2, 2>(in, out, H, W, pitch, reps);
-    if (which == 0 || which == 8) run<8, 2, 2>(in, out, H, W, pitch, reps);
-    if (which == 0 || which == 12) run<8, 3, 2>(in, out, H, W, pitch, reps);
+    if (which == 4) run<4, 2, 2>(in, out, H, W, pitch, reps);
+
+    if (which == 16) run<4, 4, 2>(in, out, H, W, pitch, reps);
+    if (which == 20) run<4, 5, 2>(in, out, H, W, pitch, reps);
+    if (which == 164) run<4, 4, 2, 4>(in, out, H, W, pitch, reps);
+    if (which == 204) run<4, 5, 2, 4>(in, out, H, W, pitch, reps);
     CHECK(hipFree(b0));
     CHECK(hipFree(b1));
     return 0;
