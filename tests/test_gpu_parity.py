@@ -342,8 +342,10 @@ def test_flow_program_bit_exact(gpu, O, monkeypatch, env, flows, n_attr, shape):
 # lane, K = 8 / 4 passes): C5, and a pre-chain + two of four attributes diffusing + a post-
 # chain with a sink -- the non-diffusing attributes pass through every level
 WIDE_PROGRAMS = [
-    C5_FLOWS,
+    C5_FLOWS,  # its pre-chain is the ring t -> t+1 mod 4: the compile-time-chain instance
     [(2, 0, 1, 0.1), (1, 0, 0, 0.1), (1, 2, 2, 0.2), (2, 3, 1, 0.05), (2, 2, -1, 0.01)],
+    # the ring's transfers in another order: not the ring, the generic chain
+    [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:],
 ]
 
 
@@ -351,7 +353,7 @@ WIDE_PROGRAMS = [
                                  {"MM_WIDE": 1, "MM_SEG_WAVES": 0.01},
                                  {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1}],
                          ids=env_id)
-@pytest.mark.parametrize("prog", [0, 1])
+@pytest.mark.parametrize("prog", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9), (45, 700), (257, 512)])
 def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
     H, W = shape
