@@ -87,7 +87,8 @@ typedef struct mm_info {
     long long steps_done;      /* steps run since the last fill/upload */
     int fused_attrs;           /* attributes carried per fused pass */
     int steps_per_launch;      /* steps fused per kernel pass (temporal blocking): 1..10
-                                  (mm_passk_kernel), 4/8/12/16/20 (mm_wide_kernel) */
+                                  (mm_passk_kernel), 4/8/12/16/20 (mm_wide_kernel, 4/8 for
+                                  four-attribute programs); mixed plans: mm_pass_plan */
     int kernel;                /* step kernel: 0 mm_pass_kernel (one step per pass),
                                   2 mm_passk_kernel (steps_per_launch steps per pass, all
                                   levels in one wave), 3 mm_wide_kernel (steps_per_launch
@@ -219,9 +220,10 @@ int mm_point_apply_strict(mm_engine* eng, int attr, long long sx, long long sy,
  * sums of the owned cells are reduced on the device and appended to the engine's
  * history (src/Model.hpp:237-243 per-rank sum; MPI_Report); the history grows as
  * needed. Asynchronous: returns once the work is enqueued. MM_HALO_HOST engines with
- * nranks > 1 run one-pass programs only and at most info.halo_depth steps per call:
- * the caller exchanges halo_depth rows (mm_halo_export_rows / mm_halo_import_rows)
- * between calls, and the engine runs the same interior / border split as with RCCL. */
+ * nranks > 1 run exactly one kernel pass per call: nsteps must be the next length
+ * mm_pass_plan returns (at most kGhost = 20); the caller exchanges that many rows
+ * (mm_halo_export_rows / mm_halo_import_rows) between calls, and the engine runs the
+ * same interior / border split as with RCCL. */
 int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
 /* Do the one-time work of a following mm_run(eng, nsteps, reduce_every) now -- capture and
  * instantiate its hipGraph, plan its eager tail passes (loading their kernels) -- without
@@ -234,7 +236,7 @@ int mm_prepare(mm_engine* eng, long long nsteps, long long reduce_every);
 int mm_pass_plan(mm_engine* eng, long long nsteps, int* lens, int cap, int* count);
 /* The kernel a pass of k steps launches (for rooflines): *kernel 0 = one-step
  * mm_pass_kernel, 2 = mm_passk_kernel, 3 = mm_wide_kernel; *cols_per_lane = columns one
- * lane computes (2 for mm_passk_kernel, 4 or 8 for mm_wide_kernel); *strips = column
+ * lane computes (2 for mm_passk_kernel; 4, or 2 for four-attribute programs, for mm_wide_kernel); *strips = column
  * strips of the slab (0 for the one-step kernel). */
 int mm_pass_kernel(mm_engine* eng, int k, int* kernel, int* cols_per_lane, long long* strips);
 int mm_synchronize(mm_engine* eng);

@@ -269,17 +269,12 @@ struct WState {
     double acc[KW][NA];
 };
 
-#ifndef MM_CHAIN_BRANCH
-#define MM_CHAIN_BRANCH 0  // 1: transfer operands picked by scalar branches
-#endif
-
 // A transfer chain in declared order (oracle/mm_oracle.c, chain_k) on each of this lane's C
 // cells: out = r*u_a; u_a -= out; u_b += out (b < 0: the outflow leaves the system); a and
-// b are wave-uniform kernel arguments. Default: chain_k's 8-wide register vector indexed
-// with s_set_gpr_idx (two moves per operand access). MM_CHAIN_BRANCH picks the operands
-// with a scalar branch per transfer and operand instead (3 fp64 operations, no moves) --
-// 2.6x slower for C5 (profiles/r03/r3k: 51 vs 132 GCUPS at K = 4): the branches cut the
-// loop body into blocks the scheduler cannot interleave.
+// b are wave-uniform kernel arguments: chain_k's 8-wide register vector indexed with
+// s_set_gpr_idx (two moves per operand access). Picking the operands with a scalar branch
+// per transfer instead was 2.6x slower for C5 (profiles/r03/r3k: the branches cut the loop
+// body into blocks the scheduler cannot interleave).
 #ifndef MM_CHAIN_RING
 #define MM_CHAIN_RING 0  // 1: pre-chains are the ring a = t, b = t+1 mod NA (engine-checked)
 #endif
@@ -301,36 +296,6 @@ __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const sign
             const double out = r * u[t][k];
             u[t][k] = u[t][k] - out;
             u[(t + 1) % NA][k] = u[(t + 1) % NA][k] + out;
-        }
-    }
-#elif MM_CHAIN_BRANCH
-#pragma unroll
-    for (int t = 0; t < kMaxChain; ++t) {
-        if (t >= n) break;  // wave-uniform
-        const int a = __builtin_amdgcn_readfirstlane((int)ta[t]);
-        const int b = __builtin_amdgcn_readfirstlane((int)tb[t]);
-        const double r = tr[t];
-        double out[C];
-#pragma unroll
-        for (int k = 0; k < C; ++k) out[k] = 0.0;
-#pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            if (a == q) {
-                asm volatile("");
-#pragma unroll
-                for (int k = 0; k < C; ++k) {
-                    out[k] = r * u[q][k];
-                    u[q][k] = u[q][k] - out[k];
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            if (b == q) {
-                asm volatile("");
-#pragma unroll
-                for (int k = 0; k < C; ++k) u[q][k] = u[q][k] + out[k];
-            }
         }
     }
 #else

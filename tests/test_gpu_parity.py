@@ -196,7 +196,10 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1}]
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1},
+    # XCD-chunked block order (off by default): the same cells, blocks on other XCDs
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_CHUNK": 16},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_XCD_CHUNK": 2}]
 
 
 def env_id(env):
