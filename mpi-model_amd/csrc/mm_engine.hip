@@ -136,6 +136,7 @@ struct mm_engine {
     std::map<std::tuple<int, long long, long long, long long>, std::pair<hipGraphExec_t, int>> graphs;
 
     bool graphs_ok = true;      // MM_GRAPH=0 (or a refused capture) runs steps eagerly
+    long long graph_min = 16;   // steps a replayed graph holds at least (MM_GRAPH_MIN_STEPS)
     int graph_state = 0;        // 0 none yet, 1 replaying, -1 capture refused
     long long graph_launches = 0;
     int graph_count = 0;
@@ -474,13 +475,25 @@ bool passk_ok(const mm_engine* e);
 // The level-split kernel runs this pass: one attribute, one diffusion, K one of its
 // instances, MM_WIDE on.
 constexpr double kWideCells = 268435456.0;  // 2^28: 16384^2, 8192 x 32768 and up
+// Below 2^25 cells (4096^2 and down) one K = 8 pass of the level-split kernel beats
+// mm_passk_kernel's K = 7 / 8: its 4 waves share a segment's pipeline fill, so segments
+// are 2.7x longer for the same number of resident waves (1000 steps of 4096^2: 1513-1585
+// vs 1410-1443 GCUPS; one pass per step at 1024^2 / 2048^2: 4.54 / 6.39 vs 6.22 / 6.69 us,
+// profiles/r03/c2graph); 8192^2 favours mm_passk_kernel K = 7 (32.4 vs 35.0 us).
+constexpr double kWideSmallCells = 33554432.0;
+constexpr int kWideSmallAuto = 8;
+
+double slab_cells(const mm_engine* e) { return (double)e->min_rows * (double)e->d.W; }
+
+// the K = 20 planner's slabs (forced MM_WIDE=1 plans every slab that way)
+bool wide_big(const mm_engine* e) { return e->wide > 0 || slab_cells(e) >= kWideCells; }
 
 bool wide_on(const mm_engine* e) {
     // auto: several attributes always (K = 8 instead of mm_passk_kernel's 2); one attribute
-    // on slabs of >= kWideCells cells, sized by the chain's thinnest slab (rank-invariant,
-    // like every plan input)
+    // on slabs of >= kWideCells or < kWideSmallCells cells, sized by the chain's thinnest
+    // slab (rank-invariant, like every plan input)
     return e->wide > 0 ||
-           (e->wide < 0 && (e->na > 1 || (double)e->min_rows * (double)e->d.W >= kWideCells));
+           (e->wide < 0 && (e->na > 1 || slab_cells(e) >= kWideCells || slab_cells(e) < kWideSmallCells));
 }
 
 bool use_wide(const mm_engine* e, int k) {
@@ -659,9 +672,10 @@ int passk_steps(const mm_engine* e) {
     // (sized by the chain's thinnest slab, the same on every rank: every rank of a halo
     // chain must run the same passes, or the K-row exchanges would not pair up)
     // wide (mm_wide_kernel): auto K = kWideAuto
+    // (wide on a small slab: kWideSmallAuto passes, no planner)
     const int kauto = (wide_on(e) && e->na == 1)
-                          ? kWideAuto
-                          : ((double)e->min_rows * (double)e->d.W >= 134217728.0 ? 8 : 7);
+                          ? (wide_big(e) ? kWideAuto : kWideSmallAuto)
+                          : (slab_cells(e) >= 134217728.0 ? 8 : 7);
     int k1 = e->kpass > 0 ? e->kpass : kauto;
     if (!(wide_on(e) && e->na == 1)) k1 = std::min(k1, mm::kMaxSteps);  // mm_passk_kernel's K
     int k = e->na == 1 ? k1 : std::min(e->kpass_multi, mm::passk_max_steps(e->na));
@@ -752,7 +766,7 @@ int next_pass_len(const mm_engine* e, long long n) {
         return (int)std::max<long long>(1, k);
     }
     if (wide_on(e) && e->na == 1) {
-        if (e->kpass == 0 && e->plan) {
+        if (e->kpass == 0 && e->plan && wide_big(e)) {
             int cap = mm::kMaxWide;
             if (e->d.nranks > 1) cap = (int)std::min<long long>(cap, e->min_rows);
             return wide_plan_first(e, n, cap);
@@ -1048,6 +1062,10 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     // (RCCL engines replace this with the chain's true minimum below)
     e->min_rows = std::min<long long>(d.h, d.H / d.nranks);
     if (const char* g = std::getenv("MM_GRAPH")) e->graphs_ok = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MM_GRAPH_MIN_STEPS")) {
+        const long long v = std::atoll(g);
+        if (v >= 1 && v <= 256) e->graph_min = v;
+    }
     e->th = choose_th(e);
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
@@ -1336,7 +1354,7 @@ long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
     if (len > 256 || nsteps < len || !e->graphs_ok) return 0;
     long long per = len;
-    while (per < 16 && per * 2 <= nsteps) per *= 2;
+    while (per < e->graph_min && per * 2 <= nsteps) per *= 2;
     // a short run that is not a whole number of graphs becomes one graph (its passes
     // balanced, enqueue_steps), instead of graphs plus an eager tail; keyed by the buffer
     // parity like every graph, so an odd number of flips is fine

@@ -36,12 +36,12 @@ def test_bench_line_contract():
     H, W = d["config"]["grid"]
     assert abs(d["value"] - H * W / (d["ms_per_step"] * 1e-3) / 1e9) <= 0.01 * d["value"]
     assert d["config"]["workload"].startswith("c2")
-    # 4096^2: K = 7 passes, balanced (no planner on a small slab)
-    assert "3 pass(es) of 7+7+6" in d["config"]["path"], d["config"]["path"]
+    # 4096^2: K = 8 passes of mm_wide_kernel and the K = 4 rest (no planner on a small slab)
+    assert "mm_wide_kernel, 3 pass(es) of 8+8+4" in d["config"]["path"], d["config"]["path"]
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
-    assert r["steps_per_launch"] == 7 and r["algorithmic_bytes_per_launch"] == 16.0 * H * W
+    assert r["steps_per_launch"] == 8 and r["algorithmic_bytes_per_launch"] == 16.0 * H * W
     assert r["valu"]["bound"] == "valu" and 0 < r["valu"]["frac"] < 1
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1 and c["sample"]

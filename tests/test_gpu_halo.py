@@ -93,7 +93,7 @@ def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k, wide):
     assert np.array_equal(got, O.field_step(O.fill_random(H, W), 0.3, steps=steps))
 
 
-@pytest.mark.parametrize("env", [{}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8},
+@pytest.mark.parametrize("env", [{}, {"MM_WIDE": 0}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8},
                                  {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12}],
                          ids=lambda e: ",".join(f"{k[3:]}={v}" for k, v in e.items()) or "default")
 @pytest.mark.parametrize("reduce_every", [1, 3])
@@ -101,7 +101,7 @@ def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k, wide):
 def test_deep_halo_chain_step_sums(gpu, O, monkeypatch, H, W, G, reduce_every, env):
     # per-step sums of every slab (partials at partial_base offsets: interior segments
     # first, then the border blocks) summed over the slabs in rank order
-    steps = 9 if not env else 2 * env["MM_STEPS_PER_PASS"] + 1
+    steps = 2 * env["MM_STEPS_PER_PASS"] + 1 if "MM_STEPS_PER_PASS" in env else 9
     engines = make_chain(gpu, monkeypatch, H, W, G, env=env)
     try:
         for e in engines:

@@ -114,7 +114,12 @@ def test_pass_planner_plans(gpu, monkeypatch):
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [7, 7, 6]
     monkeypatch.delenv("MM_WIDE")
-    with gpu.Engine(4096, 4096) as e:  # small slab: mm_passk_kernel, K = 7, no planner
+    with gpu.Engine(4096, 4096) as e:  # small slab: mm_wide_kernel, K = 8, no planner
+        e.add_diffuse(0, RATE)
+        assert e.info()["kernel"] == 3 and e.info()["steps_per_launch"] == 8
+        assert e.pass_plan(20) == [8, 8, 4]
+        assert e.pass_plan(1000) == [8] * 125
+    with gpu.Engine(8192, 8192) as e:  # between: mm_passk_kernel, K = 7
         e.add_diffuse(0, RATE)
         assert e.info()["kernel"] == 2
         assert e.pass_plan(20) == [7, 7, 6]

@@ -186,10 +186,13 @@ def make_env_engine(gpu, monkeypatch, H, W, n_attr=1, **env):
 
 # every way the engine can run a single-diffusion program: one step per pass, and the
 # K-step overlapped-strip kernel at each K / row block / block order
-FUSE_ENVS = [{"MM_PASSK": 0}, {}] + [
-    {"MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 5, 6, 7, 8, 9, 10)
-] + [{"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0},
-     {"MM_XCD_REMAP": 1}, {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16}]
+# (the default {} on these small slabs: mm_wide_kernel K = 8 passes; MM_WIDE=0 pins
+# mm_passk_kernel)
+FUSE_ENVS = [{"MM_PASSK": 0}, {}, {"MM_WIDE": 0}] + [
+    {"MM_WIDE": 0, "MM_STEPS_PER_PASS": k} for k in (1, 2, 3, 5, 6, 7, 8, 9, 10)
+] + [{"MM_WIDE": 0, **e} for e in (
+    {"MM_SEG_WAVES": 64}, {"MM_SEG_WAVES": 0.01}, {"MM_SEG_EDGE": 1.0}, {"MM_XCD_REMAP": 1},
+    {"MM_KERNEL_VARIANT": 1}, {"MM_STEPS_PER_PASS": 3, "MM_SEG_WAVES": 16})]
 # the level-split kernel (mm_wide_kernel) at each of its K, and its plan / order knobs
 WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)] + [
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_SEG_WAVES": 64},
@@ -237,10 +240,9 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
     e.close()
 
 
-@pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 3}, {"MM_STEPS_PER_PASS": 2},
-                                 {"MM_STEPS_PER_PASS": 8}, {"MM_STEPS_PER_PASS": 6},
-                                 {"MM_STEPS_PER_PASS": 7},
-                                 {"MM_STEPS_PER_PASS": 10}, {"MM_PASSK": 0}]
+@pytest.mark.parametrize("env", [{}, {"MM_WIDE": 0}]
+                         + [{"MM_WIDE": 0, "MM_STEPS_PER_PASS": k} for k in (3, 2, 8, 6, 7, 10)]
+                         + [{"MM_PASSK": 0}]
                          + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
                          ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
@@ -310,7 +312,7 @@ def add_flows(e, flows):
 
 
 @pytest.mark.parametrize("env", [{}, {"MM_STEPS_PER_PASS": 1}, {"MM_PASSK": 0},
-                                 {"MM_SEG_WAVES": 64}], ids=env_id)
+                                 {"MM_SEG_WAVES": 64}, {"MM_WIDE": 0}], ids=env_id)
 @pytest.mark.parametrize("flows,n_attr", [
     (C5_FLOWS, 4),
     ([(1, 0, 0, 0.1), (2, 0, 1, 0.2), (1, 1, 1, 0.3)], 2),       # post-chain, then a 2nd pass
