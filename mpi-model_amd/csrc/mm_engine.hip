@@ -1347,12 +1347,13 @@ namespace {
 // A graph holds a whole number of K-step passes, an even number of buffer flips (so the
 // captured pointers are valid again) and of reduction periods (so the phase is the same at
 // every replay).
-long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every) {
+long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every,
+                    bool any = false) {
     const long long unit = steps_per_launch(e);
     const long long flips = passk_ok(e) ? 1 : (long long)e->passes.size();
     long long len = unit * ((flips % 2) ? 2 : 1);
     if (reduce_every > 0) len = len / gcd_ll(len, reduce_every) * reduce_every;
-    if (len > 256 || nsteps < len || !e->graphs_ok) return 0;
+    if (len > 256 || nsteps < len || (!e->graphs_ok && !any)) return 0;
     long long per = len;
     while (per < e->graph_min && per * 2 <= nsteps) per *= 2;
     // a short run that is not a whole number of graphs becomes one graph (its passes
@@ -1485,13 +1486,24 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
         e->hist_host += entries;
         return MM_OK;
     };
+    // eager launches plan their passes in the graph path's blocks (graph_per ignoring
+    // graphs_ok / timing), so a rank whose capture was refused, or that times its
+    // kernels, runs the same pass sequence -- the same K-row exchanges -- as the others
+    auto eager = [&](bool timed) -> int {
+        const long long pp = graph_per(e, nsteps, reduce_every, true);
+        long long d = 0;
+        if (pp > 0)
+            for (; d + pp <= nsteps; d += pp) MM_TRY(enqueue_steps(e, phase + d + 1, pp, reduce_every, timed));
+        if (d < nsteps) MM_TRY(enqueue_steps(e, phase + d + 1, nsteps - d, reduce_every, timed));
+        return MM_OK;
+    };
     if (e->timing) {  // eager launches with an event pair around each step kernel
-        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, true));
+        MM_TRY(eager(true));
         return finish();
     }
     const long long per = graph_per(e, nsteps, reduce_every);
     if (per == 0) {
-        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, false));
+        MM_TRY(eager(false));
         return finish();
     }
     hipGraphExec_t g = nullptr;
@@ -1503,7 +1515,7 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
         (void)hipGetLastError();
         e->graphs_ok = false;
         e->graph_state = -1;
-        MM_TRY(enqueue_steps(e, phase + 1, nsteps, reduce_every, false));
+        MM_TRY(eager(false));
         return finish();
     }
     e->graph_state = 1;
