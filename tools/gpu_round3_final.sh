@@ -4,5 +4,5 @@ export TMPDIR=/tmp
 D=${D:-gpurun_out/r3final}
 mkdir -p $D
 D=$D bash tools/gpu_round3l.sh || exit 1
-R=gpurun_out/prof_r3c bash tools/gpu_prof_r3.sh > $D/prof.log 2>&1 || { tail -30 $D/prof.log; exit 1; }
+R=${R:-gpurun_out/prof_r3c} bash tools/gpu_prof_r3.sh > $D/prof.log 2>&1 || { tail -30 $D/prof.log; exit 1; }
 grep -E '"(workload|kernel_name|avg_us|hbm_bytes_per_launch)"' $D/prof.log
