@@ -1220,10 +1220,10 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         wide_range(e, spl, false, A, 0, e->d.h);
         info->rows_per_wave = A.th;
         const int c = wcols(e, spl);
-        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na);
+        info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
         info->kernel = 3;
         info->seg_waves_per_cu =
-            e->bpc[0][(e->variant & 1) | wring(e)][spl] * mm::wide_waves_per_block(spl, c, e->na);
+            e->bpc[0][(e->variant & 1) | wring(e)][spl] * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);

@@ -71,7 +71,7 @@ int passk_waves_per_cu(int k, int na, bool red, int nt);
 // compile-time-chain instance).
 bool wide_has(int k, int c, int na);
 int wide_out_cols(int k, int c);
-int wide_waves_per_block(int k, int c, int na);
+int wide_waves_per_block(int k, int c, int na, bool ring);
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt);
 hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
                        int variant);

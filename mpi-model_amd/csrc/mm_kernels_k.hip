@@ -98,9 +98,10 @@ bool wide_has(int k, int c, int na) {
 
 int wide_out_cols(int k, int c) { return 64 * c - 2 * c * ((k + c - 1) / c); }
 
-int wide_waves_per_block(int k, int c, int na) {
+int wide_waves_per_block(int k, int c, int na, bool ring) {
     if (!wide_has(k, c, na)) return 0;
-    return na > 1 && k == 8 ? 8 : 4;  // mm_widea_k8: one level per wave
+    if (na > 1 && k == 8) return ring ? widear_waves_k8() : 8;  // mm_widea_k8: one level per wave
+    return 4;
 }
 
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt) {

@@ -70,6 +70,7 @@ MM_WIDEA_DECL(8)
 // four attributes whose pre-chain is the ring t -> t+1 mod 4 (mm_widear_k*.hip)
 hipError_t widear_launch_k8(int na, bool red, const PassArgs& a, hipStream_t s, int v);
 int widear_blocks_k8(int na, bool red, int nt);
+int widear_waves_k8();
 
 namespace {
 

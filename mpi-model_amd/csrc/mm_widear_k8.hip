@@ -3,10 +3,16 @@
 // post-chain (config C5's topology): the chain's operands are compile-time registers
 // instead of an indexed register vector. The engine checks the pattern (is_ring).
 #ifndef MM_WIDE_U
-#define MM_WIDE_U 2
+#define MM_WIDE_U 1
 #endif
 #ifndef MM_WIDE_B
 #define MM_WIDE_B 2
+#endif
+#ifndef MM_WIDEAR_KW
+// levels per wave (P = 8 / KW waves per workgroup): two levels on 4 waves run the C5 pass
+// in 504-512 us against 595-604 for one level on 8 (same box, bit-identical states;
+// profiles/r03/c5var); 4 waves also halve the LDS (48 KiB: two workgroups per CU)
+#define MM_WIDEAR_KW 2
 #endif
 #define MM_CHAIN_RING 1
 #include "mm_wide.hpp"
@@ -14,12 +20,14 @@
 namespace mm {
 
 hipError_t widear_launch_k8(int na, bool red, const PassArgs& a, hipStream_t s, int v) {
-    if (na == 4) return wide_launch2<2, 4, 1, 8, 2>(red, a, s, v);
+    if (na == 4) return wide_launch2<2, 4, MM_WIDEAR_KW, 8 / MM_WIDEAR_KW, 2>(red, a, s, v);
     return hipErrorInvalidValue;
 }
 
+int widear_waves_k8() { return 8 / MM_WIDEAR_KW; }
+
 int widear_blocks_k8(int na, bool red, int nt) {
-    return na == 4 ? wide_blocks<2, 4, 1, 8, 2>(red, nt) : 0;
+    return na == 4 ? wide_blocks<2, 4, MM_WIDEAR_KW, 8 / MM_WIDEAR_KW, 2>(red, nt) : 0;
 }
 
 }  // namespace mm
