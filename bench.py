@@ -172,17 +172,30 @@ def cpu_baseline_program(H, W, na, flows, seconds):
                       f"(scalar C, one core, no MPI found), {el:.1f} s"}
 
 
-def valu_roof(passes, h, W, kern_avg_ms):
-    """The K-step kernels' other roof: the steady-state loop issues, per
-    level-row of a strip, 7 fp64 VALU instructions per column of a lane (4 cycles per wave
-    on a SIMD) and 4 DPP moves (2 cycles). `passes`: (k, kernel, columns per lane, strips)
-    of every launch the timed average covers (mm_pass_kernel); a launch runs k levels over
-    every row of its strips (segment overlap, LDS hand-offs and the edge strips' slower body
-    not counted). frac: the launches' mean cycles per SIMD / the mean launch's cycles at the
-    2.4 GHz peak clock. None unless every launch is a K-step kernel."""
+def level_row_cycles(cols, n_diffuse=1, n_transfers=0, chain_kernel=0):
+    """VALU cycles one wave issues per level-row of its strip: per diffusing
+    attribute 7 fp64 instructions per column of a lane (4 cycles each on a SIMD) and the
+    two fp64 DPP neighbour moves (4 v_mov_dpp, 2 cycles each); per transfer of a chain and
+    column, 3 fp64 instructions (out = r*u_a, u_a - out, u_b + out), plus with run-time
+    operands (chain_kernel 1: register-vector indexing) two v_mov_b32 per access of u_a /
+    u_b read and written (8 per transfer and column, 2 cycles each)."""
+    diff = n_diffuse * (7 * cols * 4 + 4 * 2)
+    per_transfer = 3 * 4 + (8 * 2 if chain_kernel == 1 else 0)
+    return diff + n_transfers * cols * per_transfer
+
+
+def valu_roof(passes, h, W, kern_avg_ms, lr_cycles=None):
+    """The K-step kernels' other roof: the steady-state loop's VALU cycles
+    per SIMD. `passes`: (k, kernel, columns per lane, strips) of every launch the timed
+    average covers (mm_pass_kernel); a launch runs k levels over every row of its strips
+    (segment overlap, LDS hand-offs and the edge strips' slower body not counted), each
+    level-row costing `lr_cycles(k, cols)` (level_row_cycles; default one diffusion). frac: the
+    launches' mean cycles per SIMD / the mean launch's cycles at the 2.4 GHz peak clock.
+    None unless every launch is a K-step kernel."""
     if not passes or kern_avg_ms <= 0 or any(kern not in (2, 3) for _, kern, _, _ in passes):
         return None
-    cyc = sum(h * k * strips * (7 * cols * 4 + 4 * 2) / (256 * 4)
+    lr = lr_cycles or (lambda k, cols: level_row_cycles(cols))
+    cyc = sum(h * k * strips * lr(k, cols) / (256 * 4)
               for k, _, cols, strips in passes) / len(passes)
     return {"bound": "valu", "cycles_per_simd_per_launch": round(cyc), "peak_clock_mhz": 2400,
             "frac": round(cyc / (kern_avg_ms * 1e-3 * 2.4e9), 4)}
@@ -190,7 +203,7 @@ def valu_roof(passes, h, W, kern_avg_ms):
 
 def make_line(*, workload, wl, N, ranks, H, W, h, na, steps, warmup, el, plan, info,
               kern_ms, n_launch, timing_steps, bytes_per_launch, passes, traffic, cons, halo,
-              self_halo):
+              self_halo, lr_cycles=None, graph_captures_timed=None):
     """The driver's JSON line (no I/O): value = whole-job GCUPS = all ranks' cell-updates /
     the max-over-ranks wall time `el` of exactly `steps` steps."""
     gcups = H * W * steps / el / 1e9
@@ -250,10 +263,12 @@ def make_line(*, workload, wl, N, ranks, H, W, h, na, steps, warmup, el, plan, i
         },
         "check": {"total_rel_drift": cons},
     }
-    if na == 1:
-        v = valu_roof(passes, h, W, kern_avg_ms)
-        if v:
-            line["roofline"]["valu"] = v
+    v = valu_roof(passes, h, W, kern_avg_ms, lr_cycles)
+    if v:
+        line["roofline"]["valu"] = v
+    if graph_captures_timed is not None:
+        # graphs captured inside the timed region (0: every graph was prepared ahead)
+        line["config"]["graph_captures_timed"] = graph_captures_timed
     return line
 
 
@@ -363,6 +378,7 @@ def main():
         eng.prepare(args.steps, reduce_every)
     run(args.warmup, reduce_every)
     eng.synchronize()
+    graphs_before = eng.info()["graph_count"]
 
     # timed region: the production path
     if N > 1:
@@ -373,6 +389,7 @@ def main():
     eng.synchronize()
     sync()
     el = time.perf_counter() - t0
+    graphs_timed = eng.info()["graph_count"] - graphs_before
     if N > 1:
         dist.barrier()
         t = torch.tensor([el], dtype=torch.float64)
@@ -412,12 +429,20 @@ def main():
             key = f"{args.workload}_n{N}_k{spl}"
             if kname in pmc.get(f"{key}_kernel", ""):
                 traffic = pmc.get(f"{key}_bytes_per_launch")
+        lr = None
+        if na > 1:  # C5: four diffusions, the pre-chain's transfers (K = 8: ring instance)
+            n_diff = sum(1 for f in C5_FLOWS if f[0] == 1)
+            n_tr = sum(1 for f in C5_FLOWS if f[0] == 2)
+            ck = info["chain_kernel"]
+            lr = lambda k, cols: level_row_cycles(  # noqa: E731
+                cols, n_diff, n_tr, ck if k == info["steps_per_launch"] else 1)
         line = make_line(workload=args.workload, wl=wl, N=N, ranks={"gpus": len(set(gpus))},
                          H=H, W=W, h=h, na=na, steps=args.steps, warmup=args.warmup, el=el,
                          plan=plan, info=info, kern_ms=kern_ms, n_launch=n_launch,
                          timing_steps=reps * args.steps, bytes_per_launch=bytes_per_launch, passes=passes, traffic=traffic,
                          cons=abs(s_after - s_before) / abs(s_before), halo=args.halo,
-                         self_halo=args.self_halo)
+                         self_halo=args.self_halo, lr_cycles=lr,
+                         graph_captures_timed=None if host else graphs_timed)
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
                 if na == 1 else cpu_baseline_program(wl["rows"], W, na, C5_FLOWS,

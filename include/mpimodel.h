@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 2
+#define MM_ABI_VERSION 3
 
 enum mm_status {
     MM_OK = 0,
@@ -101,6 +101,10 @@ typedef struct mm_info {
     long long hist_entries;    /* step-sum history entries enqueued (MPI_Report) */
     char graph_note[160];      /* why capture was refused ("" otherwise) */
     int seg_waves_per_cu;      /* resident waves per CU the K-step segment plan assumes */
+    int chain_kernel;          /* transfer chains of a four-attribute mm_wide_kernel pass:
+                                  0 none / not that kernel, 1 generic (operands picked at
+                                  run time), 2 the ring t -> t+1 mod 4 with compile-time
+                                  operands */
 } mm_info;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
@@ -183,7 +187,12 @@ int mm_device_synchronize(int device);
  * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal policy)
  * override tuning; MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
- * path, result unchanged). */
+ * path, result unchanged).
+ * An RCCL chain runs in lockstep: every rank must call mm_prepare / mm_run with the same
+ * step counts and reduce_every, with the same MM_GRAPH setting and the same timing mode
+ * (mm_set_timing), so that all ranks run the same K-row exchanges and capture the same
+ * graphs at the same call (the first capture of each graph agrees on success with one
+ * all-reduce, after draining this engine's streams). */
 int mm_engine_create(const mm_desc* desc, mm_engine** out);
 int mm_engine_destroy(mm_engine* eng);
 int mm_engine_info(mm_engine* eng, mm_info* info);

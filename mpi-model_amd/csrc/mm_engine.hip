@@ -277,7 +277,8 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
     if (kpass > 0)
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else if (kpass < 0)
-        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp, e->variant | wring(e)));
+        MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp,
+                               (e->variant & 1) | wring(e)));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -839,12 +840,18 @@ long long gcd_ll(long long a, long long b) {
 // Every rank of an RCCL chain must run the same passes, or the K-row exchanges would not
 // pair up: a graph replays the passes of its length, the eager fallback plans the rest of
 // the run. So whether a capture worked is agreed over the chain (one all-reduce of a flag,
-// at the first capture of each graph: every rank captures the same keys at the same call).
+// at the first capture of each graph: every rank captures the same keys at the same call,
+// which needs the same MM_GRAPH setting, timing mode and run lengths on every rank --
+// include/mpimodel.h). The all-reduce shares the communicator with the halo send / recv
+// of earlier runs, which may still be replaying on the compute stream: both streams are
+// drained first, so no two RCCL operations of this communicator are in flight at once.
 int agree_capture(mm_engine* e, bool ok) {
     if (!e->comm || e->d.nranks <= 1) return ok ? MM_OK : MM_ERR_HIP;
     int v = ok ? 1 : 0;
     int* dv = reinterpret_cast<int*>(e->sum_tmp);
-    if (hipMemcpy(dv, &v, sizeof v, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipStreamSynchronize(e->s_comp) != hipSuccess ||
+        hipStreamSynchronize(e->s_comm) != hipSuccess ||
+        hipMemcpy(dv, &v, sizeof v, hipMemcpyHostToDevice) != hipSuccess ||
         ncclAllReduce(dv, dv, 1, ncclInt32, ncclMin, e->comm, e->s_comm) != ncclSuccess ||
         hipStreamSynchronize(e->s_comm) != hipSuccess ||
         hipMemcpy(&v, dv, sizeof v, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1104,14 +1111,6 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     const size_t per = (size_t)e->rows_alloc * (size_t)e->pitch;  // doubles per buffer
     const size_t per_al = (per + 31) / 32 * 32;                   // 256-B aligned buffers
     e->bytes = sizeof(double) * per_al * 2 * (size_t)e->na;
-    he = hipMalloc(&e->base, e->bytes);
-    if (he != hipSuccess) return cleanup(fail(MM_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he)));
-    he = hipMemset(e->base, 0, e->bytes);
-    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(he)));
-    for (int k = 0; k < 2; ++k)
-        for (int a = 0; a < e->na; ++a)
-            e->buf[k][a] = e->base + per_al * (size_t)(k * e->na + a) + mm::kGhost * e->pitch;
-
     if (hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_ready, hipEventDisableTiming) != hipSuccess ||
@@ -1120,21 +1119,33 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         hipEventCreateWithFlags(&e->ev_comm_done, hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(MM_ERR_HIP, "stream/event creation failed"));
 
+    he = hipMalloc(&e->base, e->bytes);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he)));
+    // zeroed on the compute stream: every fill, upload and pass is enqueued there (or, on
+    // the comm stream, behind an event recorded there), so they all follow it. A zeroing
+    // on the null stream would not be ordered before them -- the engine's streams are
+    // non-blocking -- and once did land after a fill on memory another engine had just
+    // freed (tests/test_gpu_parity.py::test_fill_after_freed_engine)
+    he = hipMemsetAsync(e->base, 0, e->bytes, e->s_comp);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(he)));
+    for (int k = 0; k < 2; ++k)
+        for (int a = 0; a < e->na; ++a)
+            e->buf[k][a] = e->base + per_al * (size_t)(k * e->na + a) + mm::kGhost * e->pitch;
+
     int rc = ensure_partials(e);
     if (rc != MM_OK) return cleanup(rc);
     e->hist_cap = 1 << 12;
     if (hipMalloc(&e->hist, sizeof(double) * (size_t)e->hist_cap * e->na) != hipSuccess ||
         hipMalloc(&e->hist_n, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->hist_n, 0, sizeof(unsigned long long)) != hipSuccess)
+        hipMemsetAsync(e->hist_n, 0, sizeof(unsigned long long), e->s_comp) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "history allocation failed"));
     e->sum_blocks = std::min<long long>(1024, std::max<long long>(1, d.h));
     if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "sum scratch allocation failed"));
-    // the zeroing above runs on the null stream, which the engine's non-blocking streams do
-    // not wait for: without this a fill (or a history append) could land before it and be
-    // zeroed -- it did, on memory another engine had just freed (tools/dbg_chain2.py)
-    he = hipDeviceSynchronize();
-    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipDeviceSynchronize: ") + hipGetErrorString(he)));
+    // the zeroing above is queued on the compute stream; waiting for it here keeps a
+    // failure on this call (and costs no other engine anything: only this stream)
+    he = hipStreamSynchronize(e->s_comp);
+    if (he != hipSuccess) return cleanup(fail(MM_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(he)));
 
     if (const char* sh = std::getenv("MM_SELF_HALO"))
         e->self_halo = d.nranks == 1 && d.halo_mode == MM_HALO_RCCL && std::atoi(sh) != 0;
@@ -1222,6 +1233,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         const int c = wcols(e, spl);
         info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
         info->kernel = 3;
+        if (e->na > 1) info->chain_kernel = wring(e) ? 2 : 1;
         info->seg_waves_per_cu =
             e->bpc[0][(e->variant & 1) | wring(e)][spl] * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass

@@ -5,6 +5,7 @@ here: without a GPU the engine must refuse to start (it never falls back).
 """
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -25,7 +26,7 @@ def test_library_exports_every_declared_symbol(mm):
     L = mm.lib()
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert L.mm_abi_version() == 2
+    assert L.mm_abi_version() == 3
 
 
 def test_step_count(mm, O):
@@ -167,3 +168,34 @@ def test_strict_point_decision_matches_reference(mm, name):
     g = golden(name)
     applies = mm.point_strict_applies(g["dimx"], g["dimy"], g["nworkers"], g["src_x"], g["src_y"])
     assert applies == (1 if g["changed"] else 0)
+REF_MAIN = "/root/reference/src/Main.cpp"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_MAIN), reason="the reference exists only in the "
+                    "build container (its sources and binaries do not travel to the GPU box)")
+def test_reference_main_compiles_and_links_unchanged(tmp_path):
+    """CPU side of the drop-in claim: the reference's own src/Main.cpp,
+    byte for byte (fed on stdin, so none of its directory's headers is seen), compiles
+    against mpi-model_amd/api/ and links against libmpimodel_hip.so -- the recipe of
+    mpi-model_amd/api/Makefile, into a scratch path. Running it needs the GPU; the GPU runs
+    of the drop-in use examples/drop_in_main (the binary built from the reference stays in
+    this container: .gpurunignore)."""
+    api = os.path.join(REPO, "mpi-model_amd", "api")
+    exe = str(tmp_path / "ref_main")
+    mpi = os.environ.get("MM_MPI_HOME", "/opt/conda")
+    with open(REF_MAIN, "rb") as src:
+        p = subprocess.run(
+            ["g++", "-O2", "-std=c++14", "-Wall", f"-I{api}", f"-I{REPO}/include", f"-I{mpi}/include",
+             "-x", "c++", "-", "-x", "none", os.path.join(api, "MPIImpl.cpp"), "-o", exe,
+             f"-L{REPO}/mpi-model_amd", "-lmpimodel_hip", f"{mpi}/lib/libmpicxx.so",
+             f"{mpi}/lib/libmpi.so", "-Wl,--disable-new-dtags",
+             f"-Wl,-rpath,{REPO}/mpi-model_amd:/usr/lib/x86_64-linux-gnu:/opt/rocm/lib:{mpi}/lib"],
+            stdin=src, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    assert os.path.getsize(exe) > 0
+    # every engine entry point the drop-in calls is bound from the product library
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
+                          text=True).stdout
+    assert "mm_engine_create" in syms and "mm_run" in syms
+
+

@@ -81,6 +81,30 @@ def test_valu_roof_mixed_plan():
     assert bench.valu_roof([(1, 0, 1, 0)], h, W, 0.08) is None
 
 
+def test_valu_roof_four_attributes():
+    """C5's line carries a VALU roof too: per level-row of a lane 4 diffusions (7 fp64 per
+    column + 2 fp64 DPP moves each) and 4 transfers (3 fp64 per column; with run-time
+    operands 8 more v_mov_b32) -- 352 cycles at 2 columns with the ring instance."""
+    import bench
+    assert bench.level_row_cycles(4) == 120
+    assert bench.level_row_cycles(2, 4, 4, 2) == 4 * (56 + 8) + 4 * 2 * 12 == 352
+    assert bench.level_row_cycles(2, 4, 4, 1) == 352 + 4 * 2 * 16
+    h, W = 4096, 4096
+    info = dict(INFO, chain_kernel=2, steps_per_launch=8)
+    lr = lambda k, cols: bench.level_row_cycles(cols, 4, 4, 2 if k == 8 else 1)  # noqa: E731
+    d = bench.make_line(workload="c5", wl=bench.WORKLOADS["c5"], N=1, ranks={"gpus": 1}, H=h,
+                        W=W, h=h, na=4, steps=1000, warmup=5, el=0.06, plan=[8] * 125,
+                        info=info, kern_ms=0.43 * 125, n_launch=125, timing_steps=1000,
+                        bytes_per_launch=64.0 * h * W, passes=[(8, 3, 2, 37)] * 125,
+                        traffic=None, cons=0.0, halo="rccl", self_halo=False, lr_cycles=lr,
+                        graph_captures_timed=0)
+    v = d["roofline"]["valu"]
+    want = h * 8 * 37 * 352 / 1024
+    assert v["cycles_per_simd_per_launch"] == round(want)
+    assert v["frac"] == pytest.approx(want / (0.43e-3 * 2.4e9), rel=1e-3)
+    assert d["config"]["graph_captures_timed"] == 0
+
+
 def _exchange_worker(rank, world, port, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

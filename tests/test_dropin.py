@@ -2,7 +2,9 @@
 the GPU under mpirun, and their output files are compared with the reference's.
 
 * oracle/_ref/dropin_ref_main is the reference's own src/Main.cpp, UNCHANGED, compiled
-  against our headers (mpi-model_amd/api/Makefile; built in the build container).
+  against our headers (mpi-model_amd/api/Makefile; built in the build container and kept
+  there, .gpurunignore -- on the GPU box these runs use examples/drop_in_main; the CPU test
+  tests/test_abi.py::test_reference_main_compiles_and_links_unchanged compiles and links it).
 * examples/drop_in_main.cpp is our Main.cpp-style program.
 The reference writes ../output/comm_rank%d.txt per worker plus a merged file
 (src/Model.hpp:97-131,245-260); golden sha256s come from the reference itself

@@ -174,3 +174,61 @@ def test_driver_config_full_grid(gpu, O, monkeypatch, wide, plan):
     32768^2 grid, 20 steps under the default planner -- one K = 20 pass of the level-split
     kernel -- and under MM_WIDE=0 the 10 + 10 passes round 2's driver line timed."""
     driver_run_bands(gpu, O, monkeypatch, 32768, 32768, wide, plan)
+
+
+def test_c4_production_pass_full_grid(gpu, O, monkeypatch):
+    """C4's production pass (BASELINE configs[3], 16384^2 per GPU): the K = 20 pass of the
+    level-split kernel the 1000-step line repeats (50 x 20), at full size."""
+    driver_run_bands(gpu, O, monkeypatch, 16384, 16384, 1, [20])
+
+
+def test_c3_eight_gpu_slab_shape(gpu, O, monkeypatch):
+    """The 4096 x 32768 slab one GPU of an 8-GPU c3 run holds (2^27 cells): the default
+    planner's 20 steps are mm_passk_kernel passes of 7 + 7 + 6."""
+    driver_run_bands(gpu, O, monkeypatch, 4096, 32768, 0, [7, 7, 6])
+
+
+# ---- C5 at the size it is benchmarked at (bench.py --workload c5) ------------------------
+C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
+            (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+# the ring's transfers in another order: the same four transfers, not the ring
+C5_REORDERED = [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:]
+
+
+@pytest.mark.parametrize("flows,chain", [(C5_FLOWS, 2), (C5_REORDERED, 1)],
+                         ids=["ring", "reordered"])
+def test_c5_bench_size_bit_exact(gpu, O, flows, chain):
+    """bench.py's C5 configuration at its own size (4096^2, 4 attributes, per-step sums,
+    the default engine: K = 8 passes of the level-split kernel, the bench's segment plan):
+    21 steps (8 + 8 + 4 + 1, one graph) and then 48 more replayed as 16-step hipGraphs,
+    every attribute bit-exact against the oracle's flow program, every step's sums within
+    1e-12 (src/Attribute.hpp:8-9, src/Exponencial.hpp:18-20, src/Model.hpp:88-95)."""
+    H = W = 4096
+    from test_gpu_parity import add_flows
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    with gpu.Engine(H, W, n_attr=4) as e:
+        for a in range(4):
+            e.fill_random(a, seed=O.SEED + a)
+        add_flows(e, flows)
+        info = e.info()
+        assert info["kernel"] == 3 and info["steps_per_launch"] == 8, info
+        assert info["chain_kernel"] == chain, info
+        assert e.pass_plan(21) == [8, 8, 4, 1]
+        e.run(21, reduce_every=1)
+        want, sums = O.program_step(fields, flows, steps=21, sums_per_step=True)
+        for a in range(4):
+            got = e.download(a)
+            assert np.array_equal(got, want[a]), (a, int(np.count_nonzero(got != want[a])))
+        e.run(48, reduce_every=1)
+        i1 = e.info()
+        assert i1["graph_state"] == 1 and i1["graph_launches"] >= 4, i1
+        want, sums2 = O.program_step(want, flows, steps=48, sums_per_step=True)
+        for a in range(4):
+            got = e.download(a)
+            assert np.array_equal(got, want[a]), (a, int(np.count_nonzero(got != want[a])))
+        hist = e.sums_history()
+    sums = sums + sums2
+    assert hist.shape == (69, 4)
+    for s, row in enumerate(sums):
+        for a in range(4):
+            assert abs(hist[s, a] - row[a]) <= 1e-12 * abs(row[a]), (s, a)

@@ -356,7 +356,10 @@ WIDE_PROGRAMS = [
 
 @pytest.mark.parametrize("env", [{"MM_WIDE": 1}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4},
                                  {"MM_WIDE": 1, "MM_SEG_WAVES": 0.01},
-                                 {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1}],
+                                 {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1},
+                                 # variant bits beyond 0 must not select the ring instance
+                                 # for a program that is not the ring
+                                 {"MM_WIDE": 1, "MM_KERNEL_VARIANT": 3}],
                          ids=env_id)
 @pytest.mark.parametrize("prog", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9), (45, 700), (257, 512)])
@@ -371,6 +374,7 @@ def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
         e.fill_random(a, seed=O.SEED + a)
     add_flows(e, flows)
     assert e.info()["kernel"] == 3
+    assert e.info()["chain_kernel"] == (2 if prog == 0 else 1)
     k = int(env.get("MM_STEPS_PER_PASS", 8))
     plan = e.pass_plan(steps)
     assert sum(plan) == steps and plan[0] == k
@@ -406,8 +410,9 @@ def test_fill_after_freed_engine(gpu, O):
 
 def test_large_grid_properties(gpu, O):
     # full-size checks via size-independent properties: conservation and exact
-    # mirror symmetry of the 4096^2 (config C2 shape) step, plus a row block
-    # compared with the oracle
+    # mirror symmetry of the 4096^2 (config C2 shape) step, plus the top and bottom
+    # 64-row blocks (every column: both edge strips) compared with the oracle run on
+    # the block widened by the 20-row dependency cone
     H = W = 4096
     steps = 20
     with gpu.Engine(H, W) as e:
@@ -418,6 +423,13 @@ def test_large_grid_properties(gpu, O):
         v = e.download()
         s1 = e.sums()[0]
     assert abs(s1 - s0) <= 1e-12 * s0
+    for lo, hi, blk in ((0, 64 + steps, slice(0, 64)), (H - 64 - steps, H, slice(steps, None))):
+        band = O.fill_random(H, W, lo, hi - lo)
+        for _ in range(steps):
+            vg = np.zeros((band.shape[0] + 2, W))
+            vg[1:-1] = band
+            band = O.field_step_slab(H, W, lo, vg, RATE)
+        assert np.array_equal(v[lo:hi][blk], band[blk]), lo
     v0 = O.fill_random(H, W)
     assert abs(math.fsum(v0.ravel()) - s0) <= 1e-12 * s0
     with gpu.Engine(H, W) as e:

@@ -1,0 +1,105 @@
+#!/bin/bash
+# The one GPU runner of this repository (replaces the per-round one-off scripts).
+#
+#   bash tools/gpu.sh test [pytest args]      GPU test suite (pytest -m gpu), then smoke()
+#   bash tools/gpu.sh bench WL STEPS WARMUP [bench.py args]   one bench.py line
+#   bash tools/gpu.sh lines                   every workload's bench line: the driver's
+#                                             command (c3, 20 steps) and 1000-step c2..c5
+#   bash tools/gpu.sh prof NAME WL STEPS WARMUP [bench.py args]
+#                                             rocprofv3 --kernel-trace --stats of bench.py,
+#                                             then two PMC passes (FETCH_SIZE, WRITE_SIZE),
+#                                             summarised by tools/prof_summary.py
+#   bash tools/gpu.sh selfhalo                bench.py --self-halo beside the plain run on the
+#                                             slab shapes of the N > 1 runs (price of the
+#                                             interior / border split + RCCL exchange)
+#   bash tools/gpu.sh scale WL [N...]         the driver's multi-GPU command, N = 1 2 4 8 by
+#                                             default (needs N GPUs; never run on the 1-GPU box)
+#
+# Output under $D (default gpurun_out/run). Every GPU step runs under its own time limit and
+# a failing step ends the script (no retries): read its log under $D.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+set -o pipefail
+D=${D:-gpurun_out/run}
+mkdir -p "$D"
+
+fail() { echo "FAILED: $1 (rc=$2), log $3"; tail -30 "$3"; exit 3; }
+
+gpu_test() {
+    timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 \
+        --timeout-method thread "$@" > "$D/pytest_gpu.log" 2>&1 || fail pytest $? "$D/pytest_gpu.log"
+    tail -3 "$D/pytest_gpu.log"
+    timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$D/smoke.log" 2>&1 \
+        || fail smoke $? "$D/smoke.log"
+    cat "$D/smoke.log"
+}
+
+bench() {  # WL STEPS WARMUP [args]
+    local wl=$1 steps=$2 warm=$3
+    shift 3
+    local log="$D/bench_${wl}_${steps}${TAG:+_$TAG}.log"
+    timeout -k 10 600 python3 -u bench.py --workload "$wl" --steps "$steps" --warmup "$warm" "$@" \
+        > "$log" 2>&1 || fail "bench $wl" $? "$log"
+    grep '^{' "$log"
+}
+
+lines() {
+    bench c3 20 5
+    bench c3 1000 50
+    bench c4 1000 50
+    bench c2 1000 50
+    bench c5 1000 50
+}
+
+prof() {  # NAME WL STEPS WARMUP [args]
+    local name=$1 wl=$2 steps=$3 warm=$4
+    shift 4
+    local out="$D/prof_$name" args="--workload $wl --steps $steps --warmup $warm --no-cpu-baseline $*"
+    mkdir -p "$out"
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
+        -- python3 bench.py $args > "$out/trace.log" 2>&1 || fail "prof trace $name" $? "$out/trace.log"
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run \
+        -- python3 bench.py $args > "$out/fetch.log" 2>&1 || fail "prof fetch $name" $? "$out/fetch.log"
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run \
+        -- python3 bench.py $args > "$out/write.log" 2>&1 || fail "prof write $name" $? "$out/write.log"
+    python3 tools/prof_summary.py "$out" "$wl" > "$out/summary.json" && cat "$out/summary.json"
+}
+
+selfhalo() {
+    # slab shapes of the scaling runs: c3 N = 1 / 2 / 4 / 8 (32768 columns, 32768 / 16384 /
+    # 8192 / 4096 rows) and the c4 per-GPU slab (16384^2); each plain and with the split
+    # schedule + RCCL self-exchange, 20 steps (the driver's) and 200
+    local g
+    for g in "32768 32768" "16384 32768" "8192 32768" "4096 32768" "16384 16384"; do
+        set -- $g
+        for steps in 20 200; do
+            TAG="${1}x${2}_plain" bench c3 $steps 5 --grid $1 $2 --no-cpu-baseline
+            TAG="${1}x${2}_self" bench c3 $steps 5 --grid $1 $2 --no-cpu-baseline --self-halo
+        done
+    done
+}
+
+scale() {  # WL [N...]
+    local wl=$1
+    shift
+    local ns=${*:-1 2 4 8} n
+    for n in $ns; do
+        local log="$D/scale_${wl}_n$n.log"
+        timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+            --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus "$n" \
+            --workload "$wl" --steps 20 --warmup 5 > "$log" 2>&1 || fail "scale $wl N=$n" $? "$log"
+        grep '^{' "$log"
+    done
+}
+
+cmd=${1:-test}
+shift || true
+case "$cmd" in
+    test) gpu_test "$@" ;;
+    bench) bench "$@" ;;
+    lines) lines ;;
+    prof) prof "$@" ;;
+    selfhalo) selfhalo ;;
+    scale) scale "$@" ;;
+    *) echo "unknown command $cmd"; exit 2 ;;
+esac
