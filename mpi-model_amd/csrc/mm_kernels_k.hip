@@ -8,35 +8,36 @@ namespace mm {
 namespace {
 
 // Fixed-order sums of the levels in `mask` of partials[n][k][na] -> one history entry of
-// na sums per level, slots from the device counter (graph-replayable).
-__global__ __launch_bounds__(256) void mm_finalize_levels_kernel(const double* partials,
-                                                                 long long n, int k, int na,
-                                                                 int mask, double* hist,
-                                                                 unsigned long long* hist_n,
-                                                                 long long cap) {
+// na sums per level, slots from the device counter (graph-replayable). One workgroup per
+// (level of the mask, attribute), all in parallel: workgroup b sums level j = the e-th set
+// bit of mask (e = b / na) of attribute a = b % na -- each thread a strided run of the n
+// partials, then a tree over the 256 threads (the order of the single-workgroup kernel
+// this replaces, which walked the K x NA sums one after another: 37.8 us per C5 pass,
+// profiles/r03/r3q). The slot counter is read here and advanced by mm_hist_advance_kernel.
+__global__ __launch_bounds__(256) void mm_level_sums_kernel(const double* partials, long long n,
+                                                            int k, int na, int mask,
+                                                            double* hist,
+                                                            const unsigned long long* hist_n,
+                                                            long long cap) {
     __shared__ double red[256];
-    __shared__ unsigned long long slot;
-    if (threadIdx.x == 0) slot = *hist_n;
+    const int e = (int)blockIdx.x / na, a = (int)blockIdx.x % na;
+    int j = 0;
+    for (int c = -1; j < k; ++j)
+        if (((mask >> j) & 1) && ++c == e) break;
+    double s = 0.0;
+    for (long long i = threadIdx.x; i < n; i += 256) s = s + partials[(i * k + j) * na + a];
+    red[threadIdx.x] = s;
     __syncthreads();
-    unsigned long long e = 0;
-    for (int j = 0; j < k; ++j) {
-        if (!(mask & (1 << j))) continue;
-        for (int a = 0; a < na; ++a) {
-            double s = 0.0;
-            for (long long i = threadIdx.x; i < n; i += 256) s = s + partials[(i * k + j) * na + a];
-            red[threadIdx.x] = s;
-            __syncthreads();
-            for (int m = 128; m >= 1; m >>= 1) {
-                if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
-                __syncthreads();
-            }
-            const long long idx = (long long)(slot + e);
-            if (threadIdx.x == 0 && idx < cap) hist[idx * na + a] = red[0];
-            __syncthreads();
-        }
-        ++e;
+    for (int m = 128; m >= 1; m >>= 1) {
+        if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
+        __syncthreads();
     }
-    if (threadIdx.x == 0) *hist_n = slot + e;
+    const long long idx = (long long)*hist_n + e;
+    if (threadIdx.x == 0 && idx < cap) hist[idx * na + a] = red[0];
+}
+
+__global__ void mm_hist_advance_kernel(unsigned long long* hist_n, int entries) {
+    if (threadIdx.x == 0) *hist_n = *hist_n + (unsigned long long)entries;
 }
 
 }  // namespace
@@ -44,8 +45,11 @@ __global__ __launch_bounds__(256) void mm_finalize_levels_kernel(const double* p
 hipError_t launch_finalize_levels(const double* partials, long long n, int k, int na, int mask,
                                   double* hist, unsigned long long* hist_n, long long cap,
                                   hipStream_t s) {
-    hipLaunchKernelGGL(mm_finalize_levels_kernel, dim3(1), dim3(256), 0, s, partials, n, k, na,
-                       mask, hist, hist_n, cap);
+    const int entries = __builtin_popcount((unsigned)mask);
+    if (entries == 0) return hipSuccess;
+    hipLaunchKernelGGL(mm_level_sums_kernel, dim3((unsigned)(entries * na)), dim3(256), 0, s,
+                       partials, n, k, na, mask, hist, hist_n, cap);
+    hipLaunchKernelGGL(mm_hist_advance_kernel, dim3(1), dim3(64), 0, s, hist_n, entries);
     return hipGetLastError();
 }
 
