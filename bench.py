@@ -60,6 +60,14 @@ WORKLOADS = {
 
 C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
             (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
+# other four-attribute programs for --program (measurements of the chain kernels; the C5
+# line is C5_FLOWS): the same transfers in another order, and a pass with a post-chain
+# (tests/test_gpu_parity.py WIDE_PROGRAMS[2] and [1])
+PROGRAMS = {
+    "c5": C5_FLOWS,
+    "reordered": [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:],
+    "post": [(2, 0, 1, 0.1), (1, 0, 0, 0.1), (1, 2, 2, 0.2), (2, 3, 1, 0.05), (2, 2, -1, 0.01)],
+}
 
 
 def parse():
@@ -81,6 +89,8 @@ def parse():
     ap.add_argument("--grid", type=int, nargs=2, metavar=("H", "W"),
                     help="tests: override the workload's grid")
     ap.add_argument("--dump", help="tests: save each rank's slab to DUMP.rank<r>.npy")
+    ap.add_argument("--program", default="c5", choices=sorted(PROGRAMS),
+                    help="c5 workload: the flow program (default C5's own)")
     return ap.parse_args()
 
 
@@ -180,7 +190,7 @@ def level_row_cycles(cols, n_diffuse=1, n_transfers=0, chain_kernel=0):
     operands (chain_kernel 1: register-vector indexing) two v_mov_b32 per access of u_a /
     u_b read and written (8 per transfer and column, 2 cycles each)."""
     diff = n_diffuse * (7 * cols * 4 + 4 * 2)
-    per_transfer = 3 * 4 + (8 * 2 if chain_kernel == 1 else 0)
+    per_transfer = 3 * 4 + (8 * 2 if chain_kernel == 1 else 0)  # 2 ring, 3 chain_asm: none
     return diff + n_transfers * cols * per_transfer
 
 
@@ -348,8 +358,9 @@ def main():
     na = wl["n_attr"]
     for a in range(na):
         eng.fill_random(a, seed=mm.SEED + a)
+    flows = PROGRAMS[args.program]
     if args.workload == "c5":
-        for kind, a, b, r in C5_FLOWS:
+        for kind, a, b, r in flows:
             if kind == 1:
                 eng.add_diffuse(a, r)
             else:
@@ -430,12 +441,12 @@ def main():
             if kname in pmc.get(f"{key}_kernel", ""):
                 traffic = pmc.get(f"{key}_bytes_per_launch")
         lr = None
-        if na > 1:  # C5: four diffusions, the pre-chain's transfers (K = 8: ring instance)
-            n_diff = sum(1 for f in C5_FLOWS if f[0] == 1)
-            n_tr = sum(1 for f in C5_FLOWS if f[0] == 2)
+        if na > 1:  # C5: the program's diffusions and transfers (K = 8: its chain kernel)
+            n_diff = sum(1 for f in flows if f[0] == 1)
+            n_tr = sum(1 for f in flows if f[0] == 2)
             ck = info["chain_kernel"]
             lr = lambda k, cols: level_row_cycles(  # noqa: E731
-                cols, n_diff, n_tr, ck if k == info["steps_per_launch"] else 1)
+                cols, n_diff, n_tr, ck if k == info["steps_per_launch"] else 3)
         line = make_line(workload=args.workload, wl=wl, N=N, ranks={"gpus": len(set(gpus))},
                          H=H, W=W, h=h, na=na, steps=args.steps, warmup=args.warmup, el=el,
                          plan=plan, info=info, kern_ms=kern_ms, n_launch=n_launch,
@@ -443,9 +454,11 @@ def main():
                          cons=abs(s_after - s_before) / abs(s_before), halo=args.halo,
                          self_halo=args.self_halo, lr_cycles=lr,
                          graph_captures_timed=None if host else graphs_timed)
+        if args.workload == "c5" and args.program != "c5":
+            line["config"]["program"] = f"{args.program}: {flows}"
         if N == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl["rows"], W, args.cpu_seconds) \
-                if na == 1 else cpu_baseline_program(wl["rows"], W, na, C5_FLOWS,
+                if na == 1 else cpu_baseline_program(wl["rows"], W, na, flows,
                                                      args.cpu_seconds)
         print(json.dumps(line), flush=True)
     eng.close()

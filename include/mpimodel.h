@@ -246,7 +246,8 @@ int mm_pass_plan(mm_engine* eng, long long nsteps, int* lens, int cap, int* coun
 /* The kernel a pass of k steps launches (for rooflines): *kernel 0 = one-step
  * mm_pass_kernel, 2 = mm_passk_kernel, 3 = mm_wide_kernel; *cols_per_lane = columns one
  * lane computes (2 for mm_passk_kernel; 4, or 2 for four-attribute programs, for mm_wide_kernel); *strips = column
- * strips of the slab (0 for the one-step kernel). */
+ * strips of the slab, counted in 64-lane wave columns (a mm_wide_kernel strip of several
+ * column waves counts each; 0 for the one-step kernel). */
 int mm_pass_kernel(mm_engine* eng, int k, int* kernel, int* cols_per_lane, long long* strips);
 int mm_synchronize(mm_engine* eng);
 

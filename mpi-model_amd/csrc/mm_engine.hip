@@ -116,7 +116,8 @@ struct mm_engine {
     int xcd_chunk = kXcdChunk;  // mm_wide_kernel: runs of this many strips per XCD (MM_XCD_CHUNK, 0: off)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
-    int bpc[2][4][mm::kMaxWide + 1] = {};  // wide kernel blocks/CU cache [red][nt | ring][k]
+    std::map<long long, int> bpc;  // wide kernel blocks/CU cache: (variant, red, k)
+    bool ring_ok = true;     // the ring instance for C5-shaped chains (MM_CHAIN_RING=0: off)
     bool self_halo = false;  // test mode: one RCCL rank exchanges border rows with itself
     int variant = 0;  // kernel tuning variant (MM_KERNEL_VARIANT), 0 = default
     int nstrips = 0;
@@ -251,12 +252,57 @@ int wcols(const mm_engine* e, int) { return e->na > 1 ? 2 : 4; }
 // is the ring of transfers t -> t+1 mod 4 in that order, without a post-chain (config C5's
 // topology), runs the instance with the chain's operands fixed at compile time.
 int wring(const mm_engine* e) {
-    if (e->na != 4 || e->passes.size() != 1) return 0;
+    if (!e->ring_ok || e->na != 4 || e->passes.size() != 1) return 0;
     const Pass& p = e->passes[0];
-    if ((int)p.pre.size() != e->na || !p.post.empty()) return 0;
+    if ((int)p.pre.size() != e->na || !p.post.empty() || p.diffuse_mask != 15) return 0;
     for (int t = 0; t < e->na; ++t)
         if (p.pre[t].a != t || p.pre[t].b != (t + 1) % e->na) return 0;
     return 2;
+}
+
+// Variant bits of a wide launch beyond bit 0 (mm_internal.hpp): the ring instance (2), a
+// post-chain (4), the number of diffusing attributes (bits 4-6; relabel puts them first).
+int wvar(const mm_engine* e) {
+    if (e->na == 1 || e->passes.size() != 1) return 0;
+    const Pass& p = e->passes[0];
+    return wring(e) | (p.post.empty() ? 0 : 4) | (__builtin_popcount((unsigned)p.diffuse_mask) << 4);
+}
+
+// Identity attribute permutation, packed 2 bits per slot (launch_finalize_levels).
+constexpr int kPermIdentity = 0 | 1 << 2 | 2 << 4 | 3 << 6;
+
+// A four-attribute wide pass runs an instance with its diffusing attributes first: the
+// pass's arguments are relabelled so that physical slot i holds logical attribute perm[i]
+// -- the diffusing attributes in order, then the others -- its buffers, rates and chain
+// operands with them. Returns the permutation packed like kPermIdentity, for the step
+// sums (partials come out in physical order; the history is logical).
+int relabel(const mm_engine* e, mm::PassArgs& A) {
+    if (e->na == 1) return kPermIdentity;
+    const Pass& p = e->passes[0];
+    int perm[mm::kMaxAttr], inv[mm::kMaxAttr], n = 0;
+    for (int a = 0; a < e->na; ++a)
+        if ((p.diffuse_mask >> a) & 1) perm[n++] = a;
+    const int nd = n;
+    for (int a = 0; a < e->na; ++a)
+        if (!((p.diffuse_mask >> a) & 1)) perm[n++] = a;
+    int code = 0;
+    for (int i = 0; i < e->na; ++i) {
+        inv[perm[i]] = i;
+        code |= perm[i] << (2 * i);
+        A.in[i] = e->buf[e->cur][perm[i]];
+        A.out[i] = e->buf[e->cur ^ 1][perm[i]];
+        A.drate[i] = p.drate[perm[i]];
+    }
+    A.diffuse_mask = (1 << nd) - 1;
+    for (size_t t = 0; t < p.pre.size(); ++t) {
+        A.pre_a[t] = (signed char)inv[p.pre[t].a];
+        A.pre_b[t] = (signed char)(p.pre[t].b < 0 ? -1 : inv[p.pre[t].b]);
+    }
+    for (size_t t = 0; t < p.post.size(); ++t) {
+        A.post_a[t] = (signed char)inv[p.post[t].a];
+        A.post_b[t] = (signed char)(p.post[t].b < 0 ? -1 : inv[p.post[t].b]);
+    }
+    return code;
 }
 
 // Launch a one-step pass (kpass == 0), a K-step pass (kpass = K > 0: mm_passk_kernel;
@@ -278,7 +324,7 @@ int launch_timed(mm_engine* e, bool red, const mm::PassArgs& A, long long rows, 
         MM_HIP(mm::launch_passk(kpass, e->na, red, A, e->s_comp, e->variant));
     else if (kpass < 0)
         MM_HIP(mm::launch_wide(-kpass, wcols(e, -kpass), e->na, red, A, e->s_comp,
-                               (e->variant & 1) | wring(e)));
+                               (e->variant & 1) | wvar(e)));
     else
         MM_HIP(mm::launch_pass(e->na, red, A, e->s_comp, e->variant));
     if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
@@ -498,11 +544,13 @@ bool wide_on(const mm_engine* e) {
 }
 
 bool use_wide(const mm_engine* e, int k) {
-    return wide_on(e) && passk_ok(e) && mm::wide_has(k, wcols(e, k), e->na);
+    // four attributes: a pass with at least one diffusion (the instances diffuse 1..4)
+    return wide_on(e) && passk_ok(e) && mm::wide_has(k, wcols(e, k), e->na) &&
+           (e->na == 1 || e->passes[0].diffuse_mask != 0);
 }
 
 long long nstrips_wide(const mm_engine* e, int k) {
-    const int oc = mm::wide_out_cols(k, wcols(e, k));
+    const int oc = mm::wide_out_cols(k, wcols(e, k), e->na);
     return (e->d.W + oc - 1) / oc;
 }
 
@@ -513,9 +561,9 @@ long long nstrips_wide(const mm_engine* e, int k) {
 // iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
 // profiles/r03/kernel_table).
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
-    const int nt = (e->variant & 1) | wring(e);
+    const int nt = (e->variant & 1) | wvar(e);
     const int c = wcols(e, k);
-    int& bpc = e->bpc[red ? 1 : 0][nt][k];
+    int& bpc = e->bpc[((long long)nt << 8) | (red ? 128 : 0) | k];
     if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, e->na, red, nt));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
@@ -559,13 +607,15 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     const bool red = mask != 0;
     mm::PassArgs A;
     fill_args(e, e->passes[0], A);
+    const int perm = relabel(e, A);
     A.nstrips = (int)nstrips_wide(e, k);
     A.xcd_remap = e->xcd ? e->xcd : e->xcd_chunk;  // MM_XCD_REMAP=1, else XCD chunks
-    long long total_blocks = 0;
+    long long total_blocks = 0;  // partials units: blocks x column waves
+    const int wc = mm::wide_wc(k, wcols(e, k), e->na);
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(split_begin(e, depth));
         wide_range(e, k, red, A, depth, h - depth);
-        const long long interior = A.waves_total;
+        const long long interior = A.waves_total * wc;
         mm::PassArgs B = A;
         B.xcd_remap = 0;
         B.th = B.th_edge = depth;
@@ -576,23 +626,23 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
         B.waves_total = 2 * B.waves_a;
         B.partial_base = interior;
-        MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, wring(e)));
+        MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, wvar(e)));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
         A.partial_base = 0;
         MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
-        total_blocks = interior + B.waves_total;
+        total_blocks = interior + B.waves_total * wc;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
         if (e->split) MM_TRY(unsplit_halo(e, depth));
         wide_range(e, k, red, A, 0, h);
         A.partial_base = 0;
         MM_TRY(launch_timed(e, red, A, h, time_it, -k));
-        total_blocks = A.waves_total;
+        total_blocks = A.waves_total * wc;
     }
     if (red)
         MM_HIP(mm::launch_finalize_levels(e->partials, total_blocks, k, e->na, mask, e->hist,
-                                          e->hist_n, e->hist_cap, e->s_comp));
+                                          e->hist_n, e->hist_cap, e->s_comp, perm));
     e->cur ^= 1;
     return MM_OK;
 }
@@ -637,7 +687,7 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
     }
     if (red)
         MM_HIP(mm::launch_finalize_levels(e->partials, total_waves, k, e->na, mask, e->hist,
-                                          e->hist_n, e->hist_cap, e->s_comp));
+                                          e->hist_n, e->hist_cap, e->s_comp, kPermIdentity));
     e->cur ^= 1;
     return MM_OK;
 }
@@ -1094,6 +1144,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         if (v > 0.0 && v <= 1.0) e->seg_edge = v;
     }
     if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
+    if (const char* r = std::getenv("MM_CHAIN_RING")) e->ring_ok = std::atoi(r) != 0;
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
     // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
     e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
@@ -1233,9 +1284,10 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         const int c = wcols(e, spl);
         info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
         info->kernel = 3;
-        if (e->na > 1) info->chain_kernel = wring(e) ? 2 : 1;
+        if (e->na > 1) info->chain_kernel = (wring(e) && spl == 8) ? 2 : 3;
         info->seg_waves_per_cu =
-            e->bpc[0][(e->variant & 1) | wring(e)][spl] * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
+            e->bpc[((long long)((e->variant & 1) | wvar(e)) << 8) | spl] *
+            mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
     } else if (passk_ok(e)) {  // the whole-slab segment plan of one pass
         mm::PassArgs A;
         std::memset(&A, 0, sizeof A);
@@ -1474,7 +1526,7 @@ int mm_pass_kernel(mm_engine* e, int k, int* kernel, int* cols_per_lane, long lo
     } else if (use_wide(e, k)) {
         *kernel = 3;
         *cols_per_lane = wcols(e, k);
-        *strips = nstrips_wide(e, k);
+        *strips = nstrips_wide(e, k) * mm::wide_wc(k, wcols(e, k), e->na);  // 64-lane columns
     } else {
         *kernel = 2;
         *cols_per_lane = 2;

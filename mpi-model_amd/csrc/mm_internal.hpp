@@ -68,18 +68,23 @@ int passk_waves_per_cu(int k, int na, bool red, int nt);
 // BLOCKS), a.nstrips = ceil(W / wide_out_cols(k, c)). red: every level's sums into
 // partials[block][k][na]. variant (and nt) bit 0: non-temporal stores; bit 1: four
 // attributes whose pre-chain is the ring t -> t+1 mod 4 and no post-chain (K = 8: the
-// compile-time-chain instance).
+// compile-time-chain instance); bit 2: the pass has a post-chain (K = 8: the instance
+// that runs one); bits 4-6: K = 8, four attributes: the pass's attributes 0..N-1 diffuse,
+// the others do not (the engine relabels them so; the instance has N at compile time).
 bool wide_has(int k, int c, int na);
-int wide_out_cols(int k, int c);
+// column waves per level group of the instance (partials units per block: blocks * wc)
+int wide_wc(int k, int c, int na);
+int wide_out_cols(int k, int c, int na);
 int wide_waves_per_block(int k, int c, int na, bool ring);
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt);
 hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
                        int variant);
 // Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k][na],
 // each summed in a fixed order, to the history (na sums per entry).
+// perm: partials slot i holds attribute (perm >> 2i) & 3 (relabelled passes).
 hipError_t launch_finalize_levels(const double* partials, long long n, int k, int na, int mask,
                                   double* hist, unsigned long long* hist_n, long long cap,
-                                  hipStream_t s);
+                                  hipStream_t s, int perm);
 hipError_t launch_fill(double* buf, long long pitch, long long H, long long W, long long x_init,
                        long long h, int mode, double value, unsigned long long seed, hipStream_t s);
 hipError_t launch_point(double* buf, long long pitch, long long H, long long W, long long x_init,

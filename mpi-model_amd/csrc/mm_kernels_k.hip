@@ -14,11 +14,12 @@ namespace {
 // partials, then a tree over the 256 threads (the order of the single-workgroup kernel
 // this replaces, which walked the K x NA sums one after another: 37.8 us per C5 pass,
 // profiles/r03/r3q). The slot counter is read here and advanced by mm_hist_advance_kernel.
+// Partials slot a holds attribute (perm >> 2a) & 3 (the engine's relabelled passes).
 __global__ __launch_bounds__(256) void mm_level_sums_kernel(const double* partials, long long n,
                                                             int k, int na, int mask,
                                                             double* hist,
                                                             const unsigned long long* hist_n,
-                                                            long long cap) {
+                                                            long long cap, int perm) {
     __shared__ double red[256];
     const int e = (int)blockIdx.x / na, a = (int)blockIdx.x % na;
     int j = 0;
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(256) void mm_level_sums_kernel(const double* partia
         __syncthreads();
     }
     const long long idx = (long long)*hist_n + e;
-    if (threadIdx.x == 0 && idx < cap) hist[idx * na + a] = red[0];
+    if (threadIdx.x == 0 && idx < cap) hist[idx * na + ((perm >> (2 * a)) & 3)] = red[0];
 }
 
 __global__ void mm_hist_advance_kernel(unsigned long long* hist_n, int entries) {
@@ -44,11 +45,11 @@ __global__ void mm_hist_advance_kernel(unsigned long long* hist_n, int entries) 
 
 hipError_t launch_finalize_levels(const double* partials, long long n, int k, int na, int mask,
                                   double* hist, unsigned long long* hist_n, long long cap,
-                                  hipStream_t s) {
+                                  hipStream_t s, int perm) {
     const int entries = __builtin_popcount((unsigned)mask);
     if (entries == 0) return hipSuccess;
     hipLaunchKernelGGL(mm_level_sums_kernel, dim3((unsigned)(entries * na)), dim3(256), 0, s,
-                       partials, n, k, na, mask, hist, hist_n, cap);
+                       partials, n, k, na, mask, hist, hist_n, cap, perm);
     hipLaunchKernelGGL(mm_hist_advance_kernel, dim3(1), dim3(64), 0, s, hist_n, entries);
     return hipGetLastError();
 }
@@ -100,19 +101,61 @@ bool wide_has(int k, int c, int na) {
     return c == 4 && (k == 4 || k == 8 || k == 12 || k == 16 || k == 20);
 }
 
-int wide_out_cols(int k, int c) { return 64 * c - 2 * c * ((k + c - 1) / c); }
+int wide_wc(int k, int c, int na) {
+    if (!wide_has(k, c, na) || na > 1) return 1;
+    switch (k) {
+        case 4: return wide_wc_k4();
+        case 8: return wide_wc_k8();
+        case 12: return wide_wc_k12();
+        case 16: return wide_wc_k16();
+        default: return wide_wc_k20();
+    }
+}
+
+int wide_out_cols(int k, int c, int na) {
+    // WCols of the instance: one attribute runs K / 4 levels per wave (4 level groups)
+    const int wc = wide_wc(k, c, na);
+    const int lh = (k + c - 1) / c, kw = na > 1 ? 2 : k / 4;
+    const int lhw = wc > 1 ? (kw + c - 1) / c : 0;
+    return c * (64 - 2 * lhw) * (wc - 1) + 64 * c - 2 * c * lh;
+}
 
 int wide_waves_per_block(int k, int c, int na, bool ring) {
     if (!wide_has(k, c, na)) return 0;
-    if (na > 1 && k == 8) return ring ? widear_waves_k8() : 8;  // mm_widea_k8: one level per wave
-    return 4;
+    if (na > 1 && k == 8 && ring) return widear_waves_k8();
+    // one attribute: K / 4 levels per wave, 4 level groups x wide_wc column waves; four
+    // attributes: mm_widea_k4 1 level per wave, mm_widea_k8 2
+    return 4 * wide_wc(k, c, na);
 }
+
+namespace {
+
+// The K = 8 four-attribute instance of a variant: (nd - 1) * 2 + post, -1 if none.
+int widea8_index(int variant) {
+    const int nd = (variant >> 4) & 7, post = (variant >> 2) & 1;
+    return nd >= 1 && nd <= 4 ? (nd - 1) * 2 + post : -1;
+}
+
+}  // namespace
 
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt) {
     if (!wide_has(k, c, na)) return 0;
     if (na > 1 && k == 8 && (nt & 2)) return widear_blocks_k8(na, red, nt & 1);
+    if (na > 1 && k == 4) return widea_blocks_k4(na, red, nt & 1);
+    if (na > 1) {
+        switch (widea8_index(nt)) {
+            case 0: return widea8_blocks_n1_p0(red);
+            case 1: return widea8_blocks_n1_p1(red);
+            case 2: return widea8_blocks_n2_p0(red);
+            case 3: return widea8_blocks_n2_p1(red);
+            case 4: return widea8_blocks_n3_p0(red);
+            case 5: return widea8_blocks_n3_p1(red);
+            case 6: return widea8_blocks_n4_p0(red);
+            case 7: return widea8_blocks_n4_p1(red);
+            default: return 0;
+        }
+    }
     nt &= 1;
-    if (na > 1) return k == 4 ? widea_blocks_k4(na, red, nt) : widea_blocks_k8(na, red, nt);
     switch (k) {
         case 4: return wide_blocks_k4(red, nt);
         case 8: return wide_blocks_k8(red, nt);
@@ -127,9 +170,20 @@ hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStr
     if (a.waves_total <= 0) return hipSuccess;
     if (!wide_has(k, c, na)) return hipErrorInvalidValue;
     if (na > 1 && k == 8 && (variant & 2)) return widear_launch_k8(na, red, a, s, variant & 1);
-    if (na > 1)
-        return k == 4 ? widea_launch_k4(na, red, a, s, variant)
-                      : widea_launch_k8(na, red, a, s, variant);
+    if (na > 1 && k == 4) return widea_launch_k4(na, red, a, s, variant & 1);
+    if (na > 1) {
+        switch (widea8_index(variant)) {
+            case 0: return widea8_launch_n1_p0(red, a, s);
+            case 1: return widea8_launch_n1_p1(red, a, s);
+            case 2: return widea8_launch_n2_p0(red, a, s);
+            case 3: return widea8_launch_n2_p1(red, a, s);
+            case 4: return widea8_launch_n3_p0(red, a, s);
+            case 5: return widea8_launch_n3_p1(red, a, s);
+            case 6: return widea8_launch_n4_p0(red, a, s);
+            case 7: return widea8_launch_n4_p1(red, a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (k) {
         case 4: return wide_launch_k4(red, a, s, variant);
         case 8: return wide_launch_k8(red, a, s, variant);

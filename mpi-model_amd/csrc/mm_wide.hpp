@@ -53,20 +53,32 @@ namespace mm {
 // per-K entry points (mm_wide_k*.hip: one attribute, C = 4)
 #define MM_WIDE_DECL(K)                                                                    \
     hipError_t wide_launch_k##K(bool red, const PassArgs& a, hipStream_t s, int v);       \
-    int wide_blocks_k##K(bool red, int nt);
+    int wide_blocks_k##K(bool red, int nt);                                                \
+    int wide_wc_k##K();
 MM_WIDE_DECL(4)
 MM_WIDE_DECL(8)
 MM_WIDE_DECL(12)
 MM_WIDE_DECL(16)
 MM_WIDE_DECL(20)
 #undef MM_WIDE_DECL
-// several attributes (mm_widea_k*.hip): 2 columns per lane
-#define MM_WIDEA_DECL(K)                                                                   \
-    hipError_t widea_launch_k##K(int na, bool red, const PassArgs& a, hipStream_t s, int v); \
-    int widea_blocks_k##K(int na, bool red, int nt);
-MM_WIDEA_DECL(4)
-MM_WIDEA_DECL(8)
-#undef MM_WIDEA_DECL
+// four attributes, 2 columns per lane. K = 4 (mm_widea_k4.hip): any pass.
+hipError_t widea_launch_k4(int na, bool red, const PassArgs& a, hipStream_t s, int v);
+int widea_blocks_k4(int na, bool red, int nt);
+// K = 8 (mm_widea_k8.hip, one object per instance): the first N attributes diffuse (the
+// engine relabels the attributes so that the diffusing ones come first), with (P = 1) or
+// without (P = 0) a post-chain; non-temporal stores.
+#define MM_WIDEA8_DECL(N, P)                                                               \
+    hipError_t widea8_launch_n##N##_p##P(bool red, const PassArgs& a, hipStream_t s);     \
+    int widea8_blocks_n##N##_p##P(bool red);
+MM_WIDEA8_DECL(1, 0)
+MM_WIDEA8_DECL(2, 0)
+MM_WIDEA8_DECL(3, 0)
+MM_WIDEA8_DECL(4, 0)
+MM_WIDEA8_DECL(1, 1)
+MM_WIDEA8_DECL(2, 1)
+MM_WIDEA8_DECL(3, 1)
+MM_WIDEA8_DECL(4, 1)
+#undef MM_WIDEA8_DECL
 // four attributes whose pre-chain is the ring t -> t+1 mod 4 (mm_widear_k*.hip)
 hipError_t widear_launch_k8(int na, bool red, const PassArgs& a, hipStream_t s, int v);
 int widear_blocks_k8(int na, bool red, int nt);
@@ -89,6 +101,26 @@ namespace {
 #ifndef MM_WIDE_ASC
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
+#ifndef MM_WIDE_WC
+#define MM_WIDE_WC 1  // column waves per level group (one attribute): WC strips side by side
+#endif                // share one workgroup, their internal edges mended at every hand-off
+
+// Column waves (MM_WIDE_WC = WC > 1). A workgroup holds WC waves per level group, side by
+// side: wave (p, c) loads / computes the 64*C columns from its span's first column +
+// c * WSTEP. Inside a wave the DPP neighbour of its edge lanes is 0, so after the KW levels
+// of a group its LHW = ceil(KW / C) edge lanes next to another column wave are spoiled --
+// the overlap of 2 * LHW lanes between neighbours covers them: at the LDS hand-off a wave
+// of the next group reads those lanes from its neighbour's row instead (WCtx::rdelta).
+// Only the span's two outer edges lose K columns to the halo, so a workgroup outputs
+// WSTEP * (WC - 1) + 64C - 2C * LH columns (WC = 2, K = 20: 456 of 512 loaded = 89 %,
+// against 216 of 256 = 84 % for one wave per group).
+template <int C, int KW, int K, int WC>
+struct WCols {
+    static constexpr int LH = (K + C - 1) / C;                   // outer halo lanes per side
+    static constexpr int LHW = WC > 1 ? (KW + C - 1) / C : 0;    // spoiled lanes per inner edge
+    static constexpr int WSTEP = C * (64 - 2 * LHW);             // columns between column waves
+    static constexpr int OC = WSTEP * (WC - 1) + 64 * C - 2 * C * LH;  // output columns
+};
 
 // Iterations between two consecutive levels' first inputs: 3 with the pend hand-off (level
 // q+1 takes level q's row of the previous iteration: the KW level chains of one iteration
@@ -257,9 +289,12 @@ struct WCtx {
     __amdgpu_buffer_rsrc_t in[NA], out[NA];
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
+    int rdelta;           // WC > 1: dv2 offset of this lane's read (the neighbour wave's row)
     double* partials;
     long long pbase;
     const PassArgs* A;    // transfer chains (NA > 1)
+    // MM_CHAIN_ASM: register offsets of the pre / post chains' operands (chain_asm)
+    int pia[kMaxChain], pib[kMaxChain], qia[kMaxChain], qib[kMaxChain];
 };
 
 template <int C, int NA, int KW, int U>
@@ -279,6 +314,77 @@ struct WState {
 #ifndef MM_CHAIN_RING
 #define MM_CHAIN_RING 0  // 1: pre-chains are the ring a = t, b = t+1 mod NA (engine-checked)
 #endif
+#ifndef MM_CHAIN_ASM
+#define MM_CHAIN_ASM 0  // 1: any chain, operands indexed in the VGPR file (chain_asm)
+#endif
+#ifndef MM_ND
+#define MM_ND 0  // N > 0: attributes 0..N-1 diffuse, the others pass through (engine-checked:
+#endif           // it relabels the attributes); 0: the pass's diffuse_mask at run time
+#ifndef MM_CHAIN_PRE
+#define MM_CHAIN_PRE 1  // MM_CHAIN_ASM: 0 = the instance for programs without a pre-chain
+#endif
+#ifndef MM_CHAIN_POST
+#define MM_CHAIN_POST 1  // MM_CHAIN_ASM: 0 = the instance for programs without a post-chain
+#endif
+
+typedef double dv4 __attribute__((ext_vector_type(4)));
+
+// Run-time operands at compile-time cost (four attributes, C = 2 columns per lane): each
+// column's four values sit in four consecutive register pairs, pinned to v[200:207] and
+// v[210:217] (v[208:209] / v[218:219]: a pad slot that takes outflows leaving the system
+// and the unused transfer slots), and the s_set_gpr_idx mode adds the wave-uniform
+// register offset of u_a / u_b to the fp64 instructions themselves: per transfer and
+// column the ring's 3 operations (out = r*u_a, u_a - out, u_b + out) and no moves, where
+// LLVM's own indexing moves every operand through a temporary (2 v_mov_b32 each way). The
+// first n transfer slots run. ia / ib: 2 * the attribute (register offset), 8 for the pad. The mode is switched off before the
+// block ends; M0 (which holds the offset) is not used by the rest of the kernel.
+template <int C, int NA>
+__device__ __forceinline__ void chain_asm(double (&u)[NA][C], int n, const int (&ia)[kMaxChain],
+                                          const int (&ib)[kMaxChain], const double* tr) {
+    static_assert(NA == 4 && C == 2 && kMaxChain == 4, "four attributes, two columns");
+    dv4 x = {u[0][0], u[1][0], u[2][0], u[3][0]};
+    dv4 y = {u[0][1], u[1][1], u[2][1], u[3][1]};
+    double px, py, o0, o1;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // M0: no other use in these kernels (asm checked)
+#define MM_TR(T)                                                                   \
+    "s_set_gpr_idx_on %[ia" #T "], gpr_idx(SRC0)\n\t"                              \
+    "v_mul_f64 %[o0], v[200:201], %[r" #T "]\n\t"                                  \
+    "v_mul_f64 %[o1], v[210:211], %[r" #T "]\n\t"                                  \
+    "s_set_gpr_idx_off\n\t"                                                        \
+    "s_set_gpr_idx_on %[ia" #T "], gpr_idx(SRC0,DST)\n\t"                          \
+    "v_add_f64 v[200:201], v[200:201], -%[o0]\n\t"                                 \
+    "v_add_f64 v[210:211], v[210:211], -%[o1]\n\t"                                 \
+    "s_set_gpr_idx_off\n\t"                                                        \
+    "s_set_gpr_idx_on %[ib" #T "], gpr_idx(SRC0,DST)\n\t"                          \
+    "v_add_f64 v[200:201], v[200:201], %[o0]\n\t"                                  \
+    "v_add_f64 v[210:211], v[210:211], %[o1]\n\t"                                  \
+    "s_set_gpr_idx_off\n\t"
+    // a chain of n < 4 transfers leaves the block after its last one: a scalar branch
+    // inside the asm, so the compiler's view stays one straight-line block
+#define MM_SKIP(T)                                                                 \
+    "s_cmp_le_u32 %[n], " #T "\n\t"                                               \
+    "s_cbranch_scc1 .Lmm_chain_end%=\n\t"
+    asm volatile(MM_SKIP(0) MM_TR(0) MM_SKIP(1) MM_TR(1) MM_SKIP(2) MM_TR(2) MM_SKIP(3)
+                 MM_TR(3) ".Lmm_chain_end%=:"
+                 : "+{v[200:207]}"(x), "={v[208:209]}"(px), "+{v[210:217]}"(y),
+                   "={v[218:219]}"(py), [o0] "=&v"(o0), [o1] "=&v"(o1)
+                 : [n] "s"(n), [ia0] "s"(ia[0]), [ib0] "s"(ib[0]), [r0] "s"(tr[0]),
+                   [ia1] "s"(ia[1]), [ib1] "s"(ib[1]), [r1] "s"(tr[1]),
+                   [ia2] "s"(ia[2]), [ib2] "s"(ib[2]), [r2] "s"(tr[2]),
+                   [ia3] "s"(ia[3]), [ib3] "s"(ib[3]), [r3] "s"(tr[3])
+                 : "m0", "scc");
+#undef MM_SKIP
+#undef MM_TR
+#pragma clang diagnostic pop
+    (void)px;
+    (void)py;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        u[a][0] = x[a];
+        u[a][1] = y[a];
+    }
+}
 
 template <int C, int NA>
 __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const signed char* ta,
@@ -312,12 +418,24 @@ __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const sign
 #endif
 }
 
+// The pass's pre-chain on a level's input row (NA > 1): MM_CHAIN_ASM always runs its four
+// slots (no branch in the loop body; unused slots act on the pad), the other instances
+// only when the pass has one.
+template <int C, int NA>
+__device__ __forceinline__ void pre_chain(const WCtx<C, NA>& x, double (&u)[NA][C]) {
+    if constexpr (NA > 1 && MM_CHAIN_ASM) {
+        if (MM_CHAIN_PRE) chain_asm<C, NA>(u, x.A->npre, x.pia, x.pib, x.A->pre_r);
+    } else if (NA > 1 && x.A->npre) {
+        chain_cols<C, NA>(u, x.A->npre, x.A->pre_a, x.A->pre_b, x.A->pre_r);
+    }
+}
+
 // One level, input m = 0 / 1: the pre-chain (NA > 1), then every attribute's window; an
 // attribute that does not diffuse in this pass emits nothing (s = 0, d = u).
 template <int C, int NA, int BODY>
 __device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
                                       WinC<C> (&w)[NA], double (&u)[NA][C]) {
-    if (NA > 1 && x.A->npre) chain_cols<C, NA>(u, x.A->npre, x.A->pre_a, x.A->pre_b, x.A->pre_r);
+    pre_chain<C, NA>(x, u);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (NA > 1 && !((x.dmask >> a) & 1)) {
@@ -341,7 +459,7 @@ __device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
 template <int C, int NA, int BODY>
 __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C> (&w)[NA],
                                       double (&u)[NA][C], double (&o)[NA][C]) {
-    if (NA > 1 && x.A->npre) chain_cols<C, NA>(u, x.A->npre, x.A->pre_a, x.A->pre_b, x.A->pre_r);
+    pre_chain<C, NA>(x, u);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (NA > 1 && !((x.dmask >> a) & 1)) {
@@ -356,8 +474,11 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
             wemit<C, BODY>(x.c, x.r[a], x.r8[a], gx, w[a], u[a], o[a]);
         }
     }
-    if (NA > 1 && !MM_CHAIN_RING && x.A->npost)
+    if constexpr (NA > 1 && MM_CHAIN_ASM) {
+        if (MM_CHAIN_POST) chain_asm<C, NA>(o, x.A->npost, x.qia, x.qib, x.A->post_r);
+    } else if (NA > 1 && !MM_CHAIN_RING && x.A->npost) {
         chain_cols<C, NA>(o, x.A->npost, x.A->post_a, x.A->post_b, x.A->post_r);
+    }
 }
 
 // One iteration i of a wave (local iteration t = i - start): input row -> its KW levels
@@ -417,7 +538,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
             for (int h = 0; h < H2; ++h) {
-                const dv2 v = src[64 * (a * H2 + h) + x.lane];
+                const dv2 v = src[64 * (a * H2 + h) + x.lane + x.rdelta];
                 cur[a][2 * h] = v.x;
                 cur[a][2 * h + 1] = v.y;
             }
@@ -592,7 +713,7 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
     wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
-    if (RED) {  // partials[partial_base + block][K][NA]: this wave's KW levels
+    if (RED) {  // partials[partial_base + unit][K][NA], unit = block * WC + c: this wave's KW levels
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
 #pragma unroll
@@ -640,18 +761,22 @@ __host__ __device__ inline long long wide_grid(const PassArgs& A) {
 // one workgroup (P waves) per strip segment, C columns per lane, MW waves per SIMD. The
 // segment map is mm_passk.hpp's seg_map with blocks in place of waves: the two edge strips
 // first (A.th_edge rows), then the others (A.th rows). RED: every level's sums of the
-// block's output cells into partials[partial_base + block][K][NA]. NT & 1: non-temporal
-// stores.
+// block's output cells into partials[partial_base + block * WC + column wave][K][NA]. NT & 1:
+// non-temporal stores. MM_WIDE_WC column waves per level group (WCols).
 template <int C, int NA, int KW, int P, int MW, int U, int B, bool RED, int NT>
-__global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
+__global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const PassArgs A) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
-    constexpr int LH = (K + C - 1) / C;  // halo lanes per side
-    constexpr int OC = 64 * C - 2 * C * LH;  // output columns per strip
-    __shared__ dv2 lds[P > 1 ? P - 1 : 1][G::RL][32 * C * NA];
+    constexpr int WC = MM_WIDE_WC;
+    using WL = WCols<C, KW, K, WC>;
+    constexpr int LH = WL::LH;  // halo lanes per side
+    constexpr int OC = WL::OC;  // output columns per strip
+    constexpr int RW = 32 * C * NA;  // dv2 per LDS row
+    __shared__ dv2 lds[P > 1 ? P - 1 : 1][WC][G::RL][RW];
     __shared__ dv2 lds_x[WXpose<C>::on ? 2 : 1][WXpose<C>::on ? 32 * C : 1];
     const int lane = threadIdx.x & 63;
-    const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = wv / WC, cw = wv % WC;  // level group, column wave
     long long blk = blockIdx.x;
     if (A.xcd_remap == 1) {
         const long long per = gridDim.x / 8;
@@ -684,10 +809,14 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     int strip;
     seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, strip, x.rA, x.rB);
     const long long W = A.W;
-    const long long c0 = (long long)strip * OC - C * LH;  // first loaded column
+    // first loaded column of this wave: the strip's span starts C * LH columns before its
+    // first output column, column wave cw WSTEP columns further per wave
+    const long long c0 = (long long)strip * OC - C * LH + (long long)cw * WL::WSTEP;
     const long long y0 = c0 + C * lane;
     const bool in_row = y0 >= 0 && y0 < A.pitch;  // y0 % C == 0, pitch % 128 == 0
-    const bool store_lane = lane >= LH && lane < 64 - LH && y0 < W;
+    // output lanes: inside the outer halo, and at an inner edge up to the neighbour's
+    const int slo = cw == 0 ? LH : WL::LHW, shi = cw == WC - 1 ? 64 - LH : 64 - WL::LHW;
+    const bool store_lane = lane >= slo && lane < shi && y0 < W;
     x.voff = in_row ? (unsigned)(y0 * 8) : kOOBk;
     // columns past W inside the pitch are padding: writing them is harmless
     x.soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
@@ -714,7 +843,10 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     x.p = p;
     x.lane = lane;
     x.start = p * G::D;
-    x.dmask = A.diffuse_mask;
+    // MM_ND: the diffusion mask at compile time -- the per-attribute pass-through branch of
+    // lfill / lemit folds away (C5: 262 -> 290 GCUPS with run-time chain operands, 294 ->
+    // 312 with the ring's, profiles/r04/r4e)
+    x.dmask = MM_ND ? (1 << MM_ND) - 1 : A.diffuse_mask;
     x.g0 = A.x_init + x.rA - K;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -724,11 +856,30 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
                             A.pitch);
         x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
     }
-    x.lds_in = p > 0 ? &lds[p - 1][0][0] : &lds[0][0][0];
-    x.lds_out = p < P - 1 ? &lds[p][0][0] : &lds[0][0][0];
+    x.lds_in = p > 0 ? &lds[p - 1][cw][0][0] : &lds[0][0][0][0];
+    x.lds_out = p < P - 1 ? &lds[p][cw][0][0] : &lds[0][0][0][0];
+    // inner-edge lanes read the row the neighbouring column wave wrote (same slot and
+    // piece, 64 - 2 LHW lanes over, one region of RL rows further / back)
+    x.rdelta = 0;
+    if (WC > 1 && p > 0) {
+        if (cw > 0 && lane < WL::LHW)
+            x.rdelta = -G::RL * RW + (64 - 2 * WL::LHW);
+        else if (cw < WC - 1 && lane >= 64 - WL::LHW)
+            x.rdelta = G::RL * RW - (64 - 2 * WL::LHW);
+    }
     x.partials = A.partials;
     x.pbase = A.partial_base;
     x.A = &A;
+    if (MM_CHAIN_ASM) {  // register offsets of the chains' operands: 2 * attribute, 8 = pad
+#pragma unroll
+        for (int t = 0; t < kMaxChain; ++t) {
+            const bool pu = t < A.npre, qu = t < A.npost;
+            x.pia[t] = pu ? 2 * A.pre_a[t] : 8;
+            x.pib[t] = pu && A.pre_b[t] >= 0 ? 2 * A.pre_b[t] : 8;
+            x.qia[t] = qu ? 2 * A.post_a[t] : 8;
+            x.qib[t] = qu && A.post_b[t] >= 0 ? 2 * A.post_b[t] : 8;
+        }
+    }
 
     // every wave runs to iteration iend (a whole number of groups): the last wave emits
     // the segment's last row at iteration (P-1)*D + S0 + R - 1
@@ -737,17 +888,18 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     // a strip whose loaded columns include the grid's first / last column or columns past
     // it fixes up the lanes holding them
     const bool edge = !(c0 >= 1 && c0 + 64 * C <= W - 1);
+    // partials unit of this wave: block * WC + column wave
     if (edge)
-        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, blk, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, blk * WC + cw, iend);
     else
-        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, blk, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, blk * WC + cw, iend);
 }
 
 template <int C, int NA, int KW, int P, int MW, int NT>
 hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     constexpr int U = MM_WIDE_U;
     const long long blocks = wide_grid(a);
-    const dim3 g((unsigned)blocks), b(64 * P);
+    const dim3 g((unsigned)blocks), b(64 * P * MM_WIDE_WC);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
         hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, true, NT>), g, b, 0, s, a);
@@ -778,7 +930,7 @@ int wide_blocks_v() {
     }
     const int regs = (fa.numRegs + 7) / 8 * 8;
     const int waves_per_simd = regs > 0 ? std::min(8, 512 / regs) : 8;
-    int blocks = waves_per_simd * 4 / P;
+    int blocks = waves_per_simd * 4 / (P * MM_WIDE_WC);
     if (fa.sharedSizeBytes > 0) blocks = std::min(blocks, (int)(160 * 1024 / fa.sharedSizeBytes));
     return std::max(blocks, 0);
 }

@@ -19,4 +19,6 @@ hipError_t wide_launch_k20(bool red, const PassArgs& a, hipStream_t s, int v) {
 
 int wide_blocks_k20(bool red, int nt) { return wide_blocks<4, 1, 5, 4, MM_WIDE_MIN_WAVES>(red, nt); }
 
+int wide_wc_k20() { return MM_WIDE_WC; }
+
 }  // namespace mm

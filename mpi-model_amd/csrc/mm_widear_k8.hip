@@ -1,7 +1,8 @@
 // mm_widear_k8.hip -- the four-attribute level-split K-step kernel (mm_widea_k8.hip) for
 // programs whose pre-chain is the ring of transfers t -> t+1 mod 4 and that have no
 // post-chain (config C5's topology): the chain's operands are compile-time registers
-// instead of an indexed register vector. The engine checks the pattern (is_ring).
+// instead of an indexed register vector, and every attribute diffuses. The engine checks
+// the pattern (wring).
 #ifndef MM_WIDE_U
 #define MM_WIDE_U 1
 #endif
@@ -15,6 +16,7 @@
 #define MM_WIDEAR_KW 2
 #endif
 #define MM_CHAIN_RING 1
+#define MM_ND 4  // every attribute diffuses (the engine checks)
 #include "mm_wide.hpp"
 
 namespace mm {

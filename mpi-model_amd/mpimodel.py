@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmpimodel_hip.so")
+# MM_LIB_PATH: a tuning variant of the library (tools/build_variants.sh) for A/B runs
+LIB_PATH = os.environ.get("MM_LIB_PATH") or os.path.join(HERE, "libmpimodel_hip.so")
 
 MM_OK = 0
 MM_FLOW_DIFFUSE = 1

@@ -195,9 +195,10 @@ C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
 C5_REORDERED = [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:]
 
 
-@pytest.mark.parametrize("flows,chain", [(C5_FLOWS, 2), (C5_REORDERED, 1)],
-                         ids=["ring", "reordered"])
-def test_c5_bench_size_bit_exact(gpu, O, flows, chain):
+@pytest.mark.parametrize("flows,chain,env", [(C5_FLOWS, 2, {}), (C5_REORDERED, 3, {}),
+                                             (C5_FLOWS, 3, {"MM_CHAIN_RING": "0"})],
+                         ids=["ring", "reordered", "ring_runtime_operands"])
+def test_c5_bench_size_bit_exact(gpu, O, monkeypatch, flows, chain, env):
     """bench.py's C5 configuration at its own size (4096^2, 4 attributes, per-step sums,
     the default engine: K = 8 passes of the level-split kernel, the bench's segment plan):
     21 steps (8 + 8 + 4 + 1, one graph) and then 48 more replayed as 16-step hipGraphs,
@@ -206,7 +207,11 @@ def test_c5_bench_size_bit_exact(gpu, O, flows, chain):
     H = W = 4096
     from test_gpu_parity import add_flows
     fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     with gpu.Engine(H, W, n_attr=4) as e:
+        for k in env:
+            monkeypatch.delenv(k)
         for a in range(4):
             e.fill_random(a, seed=O.SEED + a)
         add_flows(e, flows)

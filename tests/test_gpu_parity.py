@@ -319,6 +319,8 @@ def add_flows(e, flows):
     ([(2, 0, -1, 0.01), (1, 0, 0, 0.1), (1, 0, 0, 0.2)], 1),      # sink, two diffusions of a
     ([(2, 2, 0, 0.5), (1, 1, 1, 0.1), (2, 1, 2, 0.1)], 3),        # pre + post chain, one pass
     ([(1, 0, 0, 0.2), (1, 1, 1, 0.3)], 2),                        # two diffusions, one pass
+    ([(2, 0, 1, 0.1), (2, 2, 3, 0.2), (2, 3, -1, 0.05)], 4),     # four attributes, transfers only
+    ([(2, 3, 1, 0.1), (1, 3, 3, 0.2), (1, 1, 1, 0.1)], 4),       # diffusing attributes last
 ])
 @pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9)])
 def test_flow_program_bit_exact(gpu, O, monkeypatch, env, flows, n_attr, shape):
@@ -351,6 +353,13 @@ WIDE_PROGRAMS = [
     [(2, 0, 1, 0.1), (1, 0, 0, 0.1), (1, 2, 2, 0.2), (2, 3, 1, 0.05), (2, 2, -1, 0.01)],
     # the ring's transfers in another order: not the ring, the generic chain
     [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:],
+    # a self-transfer (a -> a: u_a - out, then + out), a sink, repeated operands, a post-
+    # chain of four
+    [(2, 2, 2, 0.3), (2, 0, -1, 0.02), (2, 0, 3, 0.1), (2, 3, 0, 0.2), (1, 0, 0, 0.1),
+     (1, 1, 1, 0.2), (1, 3, 3, 0.05), (2, 1, 2, 0.1), (2, 2, 1, 0.15), (2, 1, -1, 0.01),
+     (2, 3, 3, 0.5)],
+    # four diffusions, no transfer at all (every chain slot on the pad)
+    C5_FLOWS[4:],
 ]
 
 
@@ -359,9 +368,11 @@ WIDE_PROGRAMS = [
                                  {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1},
                                  # variant bits beyond 0 must not select the ring instance
                                  # for a program that is not the ring
-                                 {"MM_WIDE": 1, "MM_KERNEL_VARIANT": 3}],
+                                 {"MM_WIDE": 1, "MM_KERNEL_VARIANT": 3},
+                                 # C5's ring on the run-time-operand chain too
+                                 {"MM_WIDE": 1, "MM_CHAIN_RING": 0}],
                          ids=env_id)
-@pytest.mark.parametrize("prog", [0, 1, 2])
+@pytest.mark.parametrize("prog", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("shape", [(67, 300), (5, 130), (130, 9), (45, 700), (257, 512)])
 def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
     H, W = shape
@@ -374,8 +385,10 @@ def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
         e.fill_random(a, seed=O.SEED + a)
     add_flows(e, flows)
     assert e.info()["kernel"] == 3
-    assert e.info()["chain_kernel"] == (2 if prog == 0 else 1)
     k = int(env.get("MM_STEPS_PER_PASS", 8))
+    # K = 8: the ring instance for C5's chain, the run-time-operand chain otherwise
+    ring = prog == 0 and k == 8 and env.get("MM_CHAIN_RING", 1) != 0
+    assert e.info()["chain_kernel"] == (2 if ring else 3)
     plan = e.pass_plan(steps)
     assert sum(plan) == steps and plan[0] == k
     assert all(e.pass_kernel(p)[0] == (3 if p in (4, 8) else 2) for p in plan)
