@@ -533,14 +533,24 @@ constexpr int kWideSmallAuto = 8;
 double slab_cells(const mm_engine* e) { return (double)e->min_rows * (double)e->d.W; }
 
 // the K = 20 planner's slabs (forced MM_WIDE=1 plans every slab that way)
-bool wide_big(const mm_engine* e) { return e->wide > 0 || slab_cells(e) >= kWideCells; }
+// Slabs of 2^27 - 2^28 cells in a halo chain (the 4096 x 32768 slabs of an 8-GPU c3 run)
+// also take the K = 20 planner: with the interior / border split the level-split kernel's
+// one K = 20 pass runs 20 steps in 1.33 ms against 1.40 for mm_passk_kernel's 7 + 7 + 6
+// (2030 vs 1913 GCUPS, `bench.py --self-halo`, 3 rounds each, profiles/r04/midslab);
+// without a halo mm_passk_kernel stays ahead there (2050 vs ~1920).
+constexpr double kWideSplitCells = 134217728.0;  // 2^27
+
+bool wide_big(const mm_engine* e) {
+    return e->wide > 0 || slab_cells(e) >= kWideCells ||
+           (e->wide < 0 && e->split && e->na == 1 && slab_cells(e) >= kWideSplitCells);
+}
 
 bool wide_on(const mm_engine* e) {
     // auto: several attributes always (K = 8 instead of mm_passk_kernel's 2); one attribute
-    // on slabs of >= kWideCells or < kWideSmallCells cells, sized by the chain's thinnest
-    // slab (rank-invariant, like every plan input)
+    // on slabs of >= kWideCells or < kWideSmallCells cells, or >= kWideSplitCells with a
+    // halo, sized by the chain's thinnest slab (rank-invariant, like every plan input)
     return e->wide > 0 ||
-           (e->wide < 0 && (e->na > 1 || slab_cells(e) >= kWideCells || slab_cells(e) < kWideSmallCells));
+           (e->wide < 0 && (e->na > 1 || wide_big(e) || slab_cells(e) < kWideSmallCells));
 }
 
 bool use_wide(const mm_engine* e, int k) {

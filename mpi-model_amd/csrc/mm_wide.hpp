@@ -153,6 +153,7 @@ struct WLane {
     int cnt[C];     // neighbour counts of the columns in an interior row (8 / 5 / 0 ...)
     bool special;   // some column of this lane has cnt != 8 (edge strips only)
     bool own[C];    // output cells of this workgroup
+    double ownw[C]; // own as 1.0 / 0.0 (RED: the weights of the all-rows-owned groups)
 };
 
 // One level's window, per column: shares of the row above (sp), shares and u - out of the
@@ -487,7 +488,7 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
 // compile time (level q takes part from t = kSkew*q and emits from t = kSkew*q + 2);
 // otherwise every level emits. slot: ring slot (first wave, compile time after unrolling).
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE,
-          bool PRO>
+          bool PRO, bool OWNED = false>
 __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st, int i,
                                           int t, int slot) {
     using G = WGeom<KW, P, B>;
@@ -572,9 +573,22 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
         double o[NA][C];
         lemit<C, NA, BODY>(x, gx, st.win[q], u, o);
         if (RED) {
-            const int r = x.rA - K + m + j - 2;  // output row of level j
+            if constexpr (OWNED) {
+                // every level's row of this iteration is an output row: the lane's fixed
+                // column weights (1 owned, 0 not), one fma per column -- fma(o, 1, acc) is
+                // acc + o, fma(o, 0, acc) is acc -- instead of a select and an add
 #pragma unroll
-            for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.rA && r < x.rB, x.c, o[a]);
+                for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                    for (int k = 0; k < C; ++k)
+                        st.acc[q][a] = __builtin_fma(o[a][k], x.c.ownw[k], st.acc[q][a]);
+                    asm volatile("" : "+v"(st.acc[q][a]));
+                }
+            } else {
+                const int r = x.rA - K + m + j - 2;  // output row of level j
+#pragma unroll
+                for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.rA && r < x.rB, x.c, o[a]);
+            }
         }
         if (q == KW - 1) {
             if constexpr (kOut && WXpose<C>::on) {  // level K: output row m - 2, piece-major
@@ -640,13 +654,15 @@ __device__ __forceinline__ void group_end(int i) {
 
 // Steady groups [b0, b1) (multiples of B) of one wave, B iterations per loop trip (ring
 // slot i mod U: U divides B).
-template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE>
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE,
+          bool OWNED = false>
 __device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st,
                                             int b0, int b1) {
     for (int base = b0; base < b1; base += B) {
 #pragma unroll
         for (int tt = 0; tt < B; ++tt)
-            wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, base + tt, 0, tt % U);
+            wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false, OWNED>(x, st, base + tt, 0,
+                                                                              tt % U);
         if (P > 1) wg_sync();
     }
 }
@@ -711,7 +727,21 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
     f0 = min(f0, (long long)iend);
     f1 = max(f0, min(f1, (long long)iend));
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
-    wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
+    if (RED) {
+        // inside the interior groups, those whose every level's output row lies in
+        // [rA, rB) (level q's row: rA - K - 1 + (i - start) + p*KW - (kSkew-1) q) sum with
+        // the lanes' fixed weights (wave_iter OWNED)
+        const long long r0 = x.start + K + 1 - (long long)x.p * KW + (kSkew - 1) * (KW - 1);
+        const long long r1 = x.start + (x.rB - x.rA) + K + 1 - (long long)x.p * KW;
+        long long m0 = (r0 + B - 1) / B * B, m1 = r1 / B * B;
+        m0 = min(max(m0, f0), f1);
+        m1 = max(m0, min(m1, f1));
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)m0);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, true>(x, st, (int)m0, (int)m1);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)m1, (int)f1);
+    } else {
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
+    }
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
     if (RED) {  // partials[partial_base + unit][K][NA], unit = block * WC + c: this wave's KW levels
 #pragma unroll
@@ -839,6 +869,7 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
         x.c.cnt[k] = x.c.sy[k] ? 3 * x.c.sy[k] - 1 : 0;
         x.c.special = x.c.special || x.c.cnt[k] != 8;
         x.c.own[k] = store_lane && y0 + k < W;
+        x.c.ownw[k] = x.c.own[k] ? 1.0 : 0.0;
     }
     x.p = p;
     x.lane = lane;

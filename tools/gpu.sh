@@ -9,6 +9,8 @@
 #                                             rocprofv3 --kernel-trace --stats of bench.py,
 #                                             then two PMC passes (FETCH_SIZE, WRITE_SIZE),
 #                                             summarised by tools/prof_summary.py
+#   bash tools/gpu.sh sq NAME WL STEPS WARMUP [bench.py args]
+#                                             SQ wave-cycle split + effective clock (PMC)
 #   bash tools/gpu.sh selfhalo                bench.py --self-halo beside the plain run on the
 #                                             slab shapes of the N > 1 runs (price of the
 #                                             interior / border split + RCCL exchange)
@@ -65,6 +67,22 @@ prof() {  # NAME WL STEPS WARMUP [args]
     python3 tools/prof_summary.py "$out" "$wl" > "$out/summary.json" && cat "$out/summary.json"
 }
 
+sq() {  # NAME WL STEPS WARMUP [args]: SQ wave-cycle split + effective clock (one --pmc pass:
+        # 6 SQ + 1 GRBM counters fit gfx950's slots), after a trace run for the kernel time
+    local name=$1 wl=$2 steps=$3 warm=$4
+    shift 4
+    local out="$D/sq_$name" args="--workload $wl --steps $steps --warmup $warm --no-cpu-baseline $*"
+    mkdir -p "$out"
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
+        -- python3 bench.py $args > "$out/trace.log" 2>&1 || fail "sq trace $name" $? "$out/trace.log"
+    local avg
+    avg=$(python3 tools/prof_summary.py "$out" "$wl" | python3 -c "import json,sys; print(json.load(sys.stdin)['steady_avg_us'])")
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
+        SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc" -o run \
+        -- python3 bench.py $args > "$out/pmc.log" 2>&1 || fail "sq pmc $name" $? "$out/pmc.log"
+    python3 tools/pmc_sq_summary.py "$out/pmc" "$avg" > "$out/summary.json" && cat "$out/summary.json"
+}
+
 selfhalo() {
     # slab shapes of the scaling runs: c3 N = 1 / 2 / 4 / 8 (32768 columns, 32768 / 16384 /
     # 8192 / 4096 rows) and the c4 per-GPU slab (16384^2); each plain and with the split
@@ -99,6 +117,7 @@ case "$cmd" in
     bench) bench "$@" ;;
     lines) lines ;;
     prof) prof "$@" ;;
+    sq) sq "$@" ;;
     selfhalo) selfhalo ;;
     scale) scale "$@" ;;
     *) echo "unknown command $cmd"; exit 2 ;;
