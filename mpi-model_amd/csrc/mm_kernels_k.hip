@@ -123,6 +123,7 @@ int wide_out_cols(int k, int c, int na) {
 int wide_waves_per_block(int k, int c, int na, bool ring) {
     if (!wide_has(k, c, na)) return 0;
     if (na > 1 && k == 8 && ring) return widear_waves_k8();
+    if (na == 1 && k == 20) return wide_waves_k20();  // MM_K20_KW levels per wave
     // one attribute: K / 4 levels per wave, 4 level groups x wide_wc column waves; four
     // attributes: mm_widea_k4 1 level per wave, mm_widea_k8 2
     return 4 * wide_wc(k, c, na);

@@ -61,6 +61,7 @@ MM_WIDE_DECL(12)
 MM_WIDE_DECL(16)
 MM_WIDE_DECL(20)
 #undef MM_WIDE_DECL
+int wide_waves_k20();  // waves per workgroup of the K = 20 instance
 // four attributes, 2 columns per lane. K = 4 (mm_widea_k4.hip): any pass.
 hipError_t widea_launch_k4(int na, bool red, const PassArgs& a, hipStream_t s, int v);
 int widea_blocks_k4(int na, bool red, int nt);

@@ -9,15 +9,22 @@
 #ifndef MM_WIDE_U
 #define MM_WIDE_U 2
 #endif
+#ifndef MM_K20_KW
+#define MM_K20_KW 5  // levels per wave (20 / MM_K20_KW waves per workgroup)
+#endif
 #include "mm_wide.hpp"
 
 namespace mm {
 
 hipError_t wide_launch_k20(bool red, const PassArgs& a, hipStream_t s, int v) {
-    return wide_launch2<4, 1, 5, 4, MM_WIDE_MIN_WAVES>(red, a, s, v);
+    return wide_launch2<4, 1, MM_K20_KW, 20 / MM_K20_KW, MM_WIDE_MIN_WAVES>(red, a, s, v);
 }
 
-int wide_blocks_k20(bool red, int nt) { return wide_blocks<4, 1, 5, 4, MM_WIDE_MIN_WAVES>(red, nt); }
+int wide_blocks_k20(bool red, int nt) {
+    return wide_blocks<4, 1, MM_K20_KW, 20 / MM_K20_KW, MM_WIDE_MIN_WAVES>(red, nt);
+}
+
+int wide_waves_k20() { return 20 / MM_K20_KW * MM_WIDE_WC; }
 
 int wide_wc_k20() { return MM_WIDE_WC; }
 
