@@ -102,6 +102,9 @@ namespace {
 #ifndef MM_WIDE_ASC
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
+#ifndef MM_PROBE_L2ROWS
+#define MM_PROBE_L2ROWS 0  // timing probe (tools/build_variants.sh only): see wave_iter
+#endif
 #ifndef MM_WIDE_WC
 #define MM_WIDE_WC 1  // column waves per level group (one attribute): WC strips side by side
 #endif                // share one workgroup, their internal edges mended at every hand-off
@@ -528,7 +531,13 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
 #endif
             }
         }
+#if MM_PROBE_L2ROWS
+        // timing probe only (wrong results): the loading wave re-reads the segment's first
+        // 8 rows, L2-resident, instead of streaming -- what HBM latency costs the pass
+        const unsigned o = x.voff + (unsigned)((i + U) & 7) * x.rowb;
+#else
         const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;
+#endif
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
 #pragma unroll

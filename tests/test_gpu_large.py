@@ -182,6 +182,19 @@ def test_c4_production_pass_full_grid(gpu, O, monkeypatch):
     driver_run_bands(gpu, O, monkeypatch, 16384, 16384, 1, [20])
 
 
+def test_mid_slab_in_a_chain_takes_the_k20_planner(gpu):
+    """Slabs of 2^27 - 2^28 cells with a halo (rank 0 of an 8-rank c3 chain: 4096 x 32768)
+    plan the level-split kernel's K = 20 pass -- with the interior / border split it beats
+    mm_passk_kernel's 7 + 7 + 6 (profiles/r04/midslab); the same slab alone keeps them."""
+    with gpu.Engine(32768, 32768, 0, 4096, rank=0, nranks=8, halo_mode=gpu.MM_HALO_HOST) as e:
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [20]
+        assert e.pass_kernel(20)[0] == 3 and e.info()["halo_depth"] == 20
+    with gpu.Engine(4096, 32768) as e:
+        e.add_diffuse(0, RATE)
+        assert e.pass_plan(20) == [7, 7, 6] and e.info()["kernel"] == 2
+
+
 def test_c3_eight_gpu_slab_shape(gpu, O, monkeypatch):
     """The 4096 x 32768 slab one GPU of an 8-GPU c3 run holds (2^27 cells): the default
     planner's 20 steps are mm_passk_kernel passes of 7 + 7 + 6."""

@@ -11,6 +11,8 @@
 #                                             summarised by tools/prof_summary.py
 #   bash tools/gpu.sh sq NAME WL STEPS WARMUP [bench.py args]
 #                                             SQ wave-cycle split + effective clock (PMC)
+#   bash tools/gpu.sh pmc NAME WL STEPS WARMUP "COUNTERS" [bench.py args]
+#                                             one --pmc pass, mean counters per dispatch
 #   bash tools/gpu.sh selfhalo                bench.py --self-halo beside the plain run on the
 #                                             slab shapes of the N > 1 runs (price of the
 #                                             interior / border split + RCCL exchange)
@@ -83,6 +85,16 @@ sq() {  # NAME WL STEPS WARMUP [args]: SQ wave-cycle split + effective clock (on
     python3 tools/pmc_sq_summary.py "$out/pmc" "$avg" > "$out/summary.json" && cat "$out/summary.json"
 }
 
+pmc() {  # NAME WL STEPS WARMUP "COUNTERS" [args]: one --pmc pass of up to 8 SQ counters
+    local name=$1 wl=$2 steps=$3 warm=$4 counters=$5
+    shift 5
+    local out="$D/pmc_$name" args="--workload $wl --steps $steps --warmup $warm --no-cpu-baseline $*"
+    mkdir -p "$out"
+    timeout -s KILL 300 rocprofv3 --pmc $counters --output-format csv -d "$out/pmc" -o run \
+        -- python3 bench.py $args > "$out/pmc.log" 2>&1 || fail "pmc $name" $? "$out/pmc.log"
+    python3 tools/pmc_sq_summary.py "$out/pmc" > "$out/summary.json" && cat "$out/summary.json"
+}
+
 selfhalo() {
     # slab shapes of the scaling runs: c3 N = 1 / 2 / 4 / 8 (32768 columns, 32768 / 16384 /
     # 8192 / 4096 rows) and the c4 per-GPU slab (16384^2); each plain and with the split
@@ -118,6 +130,7 @@ case "$cmd" in
     lines) lines ;;
     prof) prof "$@" ;;
     sq) sq "$@" ;;
+    pmc) pmc "$@" ;;
     selfhalo) selfhalo ;;
     scale) scale "$@" ;;
     *) echo "unknown command $cmd"; exit 2 ;;
