@@ -124,7 +124,7 @@ struct mm_engine {
     double* partials = nullptr;
     long long partials_cap = 0;
     double* hist = nullptr;
-    unsigned long long* hist_n = nullptr;
+    unsigned long long* hist_n = nullptr;  // [0] history entries, [1] level-sum workgroups done
     long long hist_cap = 0;
     long long hist_host = 0;    // entries the enqueued work appends (host-side count)
     double* sum_tmp = nullptr;  // mm_sums scratch: nblocks partials + 1 result per attribute
@@ -1197,8 +1197,8 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (rc != MM_OK) return cleanup(rc);
     e->hist_cap = 1 << 12;
     if (hipMalloc(&e->hist, sizeof(double) * (size_t)e->hist_cap * e->na) != hipSuccess ||
-        hipMalloc(&e->hist_n, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemsetAsync(e->hist_n, 0, sizeof(unsigned long long), e->s_comp) != hipSuccess)
+        hipMalloc(&e->hist_n, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemsetAsync(e->hist_n, 0, 2 * sizeof(unsigned long long), e->s_comp) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "history allocation failed"));
     e->sum_blocks = std::min<long long>(1024, std::max<long long>(1, d.h));
     if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)

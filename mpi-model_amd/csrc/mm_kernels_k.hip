@@ -13,12 +13,14 @@ namespace {
 // bit of mask (e = b / na) of attribute a = b % na -- each thread a strided run of the n
 // partials, then a tree over the 256 threads (the order of the single-workgroup kernel
 // this replaces, which walked the K x NA sums one after another: 37.8 us per C5 pass,
-// profiles/r03/r3q). The slot counter is read here and advanced by mm_hist_advance_kernel.
-// Partials slot a holds attribute (perm >> 2a) & 3 (the engine's relabelled passes).
+// profiles/r03/r3q). Partials slot a holds attribute (perm >> 2a) & 3 (the engine's
+// relabelled passes). Every workgroup reads the slot counter hist_n[0]; the last one to
+// finish (hist_n[1] counts them, agent-scope atomics: the workgroups run on every XCD)
+// advances it and resets the count for the next launch.
 __global__ __launch_bounds__(256) void mm_level_sums_kernel(const double* partials, long long n,
                                                             int k, int na, int mask,
                                                             double* hist,
-                                                            const unsigned long long* hist_n,
+                                                            unsigned long long* hist_n,
                                                             long long cap, int perm) {
     __shared__ double red[256];
     const int e = (int)blockIdx.x / na, a = (int)blockIdx.x % na;
@@ -33,12 +35,21 @@ __global__ __launch_bounds__(256) void mm_level_sums_kernel(const double* partia
         if ((int)threadIdx.x < m) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + m];
         __syncthreads();
     }
-    const long long idx = (long long)*hist_n + e;
-    if (threadIdx.x == 0 && idx < cap) hist[idx * na + ((perm >> (2 * a)) & 3)] = red[0];
-}
-
-__global__ void mm_hist_advance_kernel(unsigned long long* hist_n, int entries) {
-    if (threadIdx.x == 0) *hist_n = *hist_n + (unsigned long long)entries;
+    if (threadIdx.x == 0) {
+        const unsigned long long slot =
+            __hip_atomic_load(hist_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long idx = (long long)slot + e;
+        if (idx < cap) hist[idx * na + ((perm >> (2 * a)) & 3)] = red[0];
+        // the slot is read before this workgroup counts itself done (acq_rel orders them)
+        const unsigned long long done = __hip_atomic_fetch_add(
+            hist_n + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (unsigned long long)gridDim.x - 1) {
+            const int entries = __builtin_popcount((unsigned)mask);
+            __hip_atomic_store(hist_n, slot + (unsigned long long)entries, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(hist_n + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace
@@ -50,7 +61,6 @@ hipError_t launch_finalize_levels(const double* partials, long long n, int k, in
     if (entries == 0) return hipSuccess;
     hipLaunchKernelGGL(mm_level_sums_kernel, dim3((unsigned)(entries * na)), dim3(256), 0, s,
                        partials, n, k, na, mask, hist, hist_n, cap, perm);
-    hipLaunchKernelGGL(mm_hist_advance_kernel, dim3(1), dim3(64), 0, s, hist_n, entries);
     return hipGetLastError();
 }
 
