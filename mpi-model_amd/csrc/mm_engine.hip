@@ -138,6 +138,7 @@ struct mm_engine {
 
     bool graphs_ok = true;      // MM_GRAPH=0 (or a refused capture) runs steps eagerly
     long long graph_min = 16;   // steps a replayed graph holds at least (MM_GRAPH_MIN_STEPS)
+    long long graph_max = 128;  // step kernels a graph holds at most (MM_GRAPH_MAX_LAUNCHES)
     int graph_state = 0;        // 0 none yet, 1 replaying, -1 capture refused
     long long graph_launches = 0;
     int graph_count = 0;
@@ -1133,6 +1134,10 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         const long long v = std::atoll(g);
         if (v >= 1 && v <= 256) e->graph_min = v;
     }
+    if (const char* g = std::getenv("MM_GRAPH_MAX_LAUNCHES")) {
+        const long long v = std::atoll(g);
+        if (v >= 1 && v <= 4096) e->graph_max = v;
+    }
     e->th = choose_th(e);
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
@@ -1434,6 +1439,20 @@ long long graph_per(const mm_engine* e, long long nsteps, long long reduce_every
     // balanced, enqueue_steps), instead of graphs plus an eager tail; keyed by the buffer
     // parity like every graph, so an odd number of flips is fine
     if (nsteps % per != 0 && nsteps <= 64 * unit) per = nsteps;
+    // fewer, longer graphs: consecutive graph launches start ~9 us apart on the GPU, the
+    // kernels inside one graph back to back (c2, 16-step graphs: 62 such gaps in 1000
+    // steps, 5 % of the run, profiles/r04/final/prof_c2_k8). So the longest whole number of
+    // base blocks (the pass length and the reduce period, so every graph starts at the
+    // same phase) that divides the run, up to graph_max step kernels
+    const long long base = reduce_every > 0 ? unit / gcd_ll(unit, reduce_every) * reduce_every : unit;
+    if (nsteps % base == 0) {
+        const long long m = nsteps / base, per_block = base / unit * flips;  // kernels per block
+        for (long long d = std::min(m, e->graph_max / per_block); d * base > per; --d)
+            if (m % d == 0) {
+                per = d * base;
+                break;
+            }
+    }
     return per;
 }
 

@@ -102,6 +102,9 @@ namespace {
 #ifndef MM_WIDE_ASC
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
+#ifndef MM_WIDE_GLDS
+#define MM_WIDE_GLDS 0  // R > 0: one attribute, the loading wave streams its input rows through
+#endif                  // an R-row LDS ring filled by LDS-DMA, R - 1 rows ahead (WGlds)
 #ifndef MM_PROBE_L2ROWS
 #define MM_PROBE_L2ROWS 0  // timing probe (tools/build_variants.sh only): see wave_iter
 #endif
@@ -146,6 +149,40 @@ template <int C>
 struct WXpose {
     static constexpr bool on = C >= 6 && MM_WIDE_XPOSE;
 };
+
+// The loading wave's input ring (MM_WIDE_GLDS = R rows, one attribute): row i of the
+// segment lands in slot i % R by global_load_lds_dwordx4 (16 B per lane, lane-linear: the
+// ring's row layout [piece][lane] is exactly that), issued R - 1 iterations ahead, so its
+// HBM latency is covered by R - 1 iterations instead of the register prefetch's U, and the
+// U prefetch registers are free. The DMAs are inline asm, outside the compiler's s_waitcnt
+// bookkeeping: the wave counts them itself (vmcnt) before it reads a slot, and it issues
+// no other vector-memory loads in its loop. Addresses have no range check (buffer loads
+// had): rows are clamped to the segment's [rA - K, rB + K), columns outside the pitch to
+// the row's first / last piece -- columns outside the grid emit nothing either way.
+template <int C, int NA>
+struct WGlds {
+    static constexpr int R = MM_WIDE_GLDS;
+    static constexpr bool on = R > 2 && NA == 1 && !WXpose<C>::on;
+    static constexpr int SLOT = (C / 2) * 64;  // dv2 per ring slot
+};
+
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 enum { kBodyFast = 0, kBodyEdge = 1, kBodyGen = 2 };
 
@@ -295,6 +332,10 @@ struct WCtx {
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
     int rdelta;           // WC > 1: dv2 offset of this lane's read (the neighbour wave's row)
+    const double* gsrc;   // WGlds: this lane's column of segment input row 0 (clamped)
+    const dv2* lds_pfr;   // WGlds: the ring (R slots of H2 x 64 dv2)
+    unsigned pf_lds;      // WGlds: LDS byte address of the ring
+    int prow_max;         // WGlds: last segment input row that exists (rB - rA + 2K - 1)
     double* partials;
     long long pbase;
     const PassArgs* A;    // transfer chains (NA > 1)
@@ -517,6 +558,25 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
         const unsigned ro = (unsigned)(i + U) * x.rowb;
 #pragma unroll
         for (int h = 0; h < H2; ++h) st.raw[slot][0][h] = load_row(x.in[0], x.xvoff[h] + ro);
+    } else if constexpr (ROLE == kRoleFirst && WGlds<C, NA>::on) {
+        // row i is in slot i % R once the DMAs issued after it (rows i+1 .. i+R-2, H2
+        // each) are all that is left in flight; then refill the slot read last iteration
+        // with row i + R - 1
+        using GL = WGlds<C, NA>;
+        constexpr int R = GL::R;
+        wait_vmcnt<(R - 2) * H2>();
+        const dv2* src = x.lds_pfr + (i % R) * GL::SLOT;
+#pragma unroll
+        for (int h = 0; h < H2; ++h) {
+            const dv2 v = src[64 * h + x.lane];
+            cur[0][2 * h] = v.x;
+            cur[0][2 * h + 1] = v.y;
+        }
+        const int nr = min(i + R - 1, x.prow_max);
+        const unsigned slot_b = x.pf_lds + (unsigned)(((i + R - 1) % R) * (GL::SLOT * 16));
+#pragma unroll
+        for (int h = 0; h < H2; ++h)
+            glds16(x.gsrc + (long long)nr * (x.rowb / 8) + 2 * h, slot_b + 1024u * h);
     } else if (kIn) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -694,6 +754,17 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
     if (kIn) {
         // start = 0: the prologue and the iterations up to the first group boundary are
         // unrolled (compile-time ring slots)
+        if constexpr (ROLE == kRoleFirst && WGlds<C, NA>::on) {  // rows 0 .. R-2 of the ring
+            using GL = WGlds<C, NA>;
+#pragma unroll
+            for (int k = 0; k < GL::R - 1; ++k) {
+                const int nr = min(k, x.prow_max);
+#pragma unroll
+                for (int h = 0; h < C / 2; ++h)
+                    glds16(x.gsrc + (long long)nr * (x.rowb / 8) + 2 * h,
+                           x.pf_lds + (unsigned)(k * GL::SLOT * 16 + 1024 * h));
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
 #pragma unroll
@@ -704,6 +775,7 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
                                           ? load_row(x.in[a], x.xvoff[h] + k * x.rowb)
                                           : load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
             }
+        }
         }
 #pragma unroll
         for (int t = 0; t < G::T0; ++t) {
@@ -814,6 +886,8 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
     constexpr int RW = 32 * C * NA;  // dv2 per LDS row
     __shared__ dv2 lds[P > 1 ? P - 1 : 1][WC][G::RL][RW];
     __shared__ dv2 lds_x[WXpose<C>::on ? 2 : 1][WXpose<C>::on ? 32 * C : 1];
+    using GL = WGlds<C, NA>;
+    __shared__ dv2 lds_g[GL::on ? GL::R * GL::SLOT : 1];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int p = wv / WC, cw = wv % WC;  // level group, column wave
@@ -907,6 +981,16 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
             x.rdelta = -G::RL * RW + (64 - 2 * WL::LHW);
         else if (cw < WC - 1 && lane >= 64 - WL::LHW)
             x.rdelta = G::RL * RW - (64 - 2 * WL::LHW);
+    }
+    if constexpr (GL::on) {
+        // the ring's DMA source: this lane's columns clamped into the row (a clamped lane
+        // holds columns outside the grid, whose cells emit nothing); LDS address = the low
+        // 32 bits of the LDS aperture address
+        const long long yc = y0 < 0 ? 0 : (y0 > A.pitch - C ? A.pitch - C : y0);
+        x.gsrc = A.in[0] + (long long)(x.rA - K) * A.pitch + yc;
+        x.lds_pfr = &lds_g[0];
+        x.pf_lds = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)&lds_g[0]);
+        x.prow_max = x.rB - x.rA + 2 * K - 1;
     }
     x.partials = A.partials;
     x.pbase = A.partial_base;

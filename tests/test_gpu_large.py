@@ -220,6 +220,9 @@ def test_c5_bench_size_bit_exact(gpu, O, monkeypatch, flows, chain, env):
     H = W = 4096
     from test_gpu_parity import add_flows
     fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    # graphs of 2 passes (the engine would take all 48 steps as one graph): replays
+    # alternating between the two buffer parities
+    env = dict(env, MM_GRAPH_MAX_LAUNCHES="2")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     with gpu.Engine(H, W, n_attr=4) as e:
@@ -239,7 +242,7 @@ def test_c5_bench_size_bit_exact(gpu, O, monkeypatch, flows, chain, env):
             assert np.array_equal(got, want[a]), (a, int(np.count_nonzero(got != want[a])))
         e.run(48, reduce_every=1)
         i1 = e.info()
-        assert i1["graph_state"] == 1 and i1["graph_launches"] >= 4, i1
+        assert i1["graph_state"] == 1 and i1["graph_launches"] >= 3, i1
         want, sums2 = O.program_step(want, flows, steps=48, sums_per_step=True)
         for a in range(4):
             got = e.download(a)

@@ -299,6 +299,35 @@ def test_fused_steps_graph_replay_many_steps(gpu, O, monkeypatch, k, wide):
         assert abs(a - b) <= 1e-12 * b
 
 
+@pytest.mark.parametrize("max_launches,launches", [(None, 1), (3, 4), (1, 6)])
+def test_graph_length_divides_run(gpu, O, monkeypatch, max_launches, launches):
+    # a run that is a whole number of passes replays as the longest graph dividing it (up
+    # to MM_GRAPH_MAX_LAUNCHES step kernels): 96 steps of K = 8 with per-step sums are one
+    # graph of 12 passes by default; 3 passes per graph (an odd number of buffer flips, so
+    # launches alternate between the two parities' graphs) replay more; a cap under the
+    # 16 steps of MM_GRAPH_MIN_STEPS leaves 2-pass graphs
+    H, W, steps = 300, 700, 96
+    env = {"MM_STEPS_PER_PASS": 8, "MM_WIDE": 1}
+    if max_launches is not None:
+        env["MM_GRAPH_MAX_LAUNCHES"] = max_launches
+    e = make_env_engine(gpu, monkeypatch, H, W, **env)
+    e.fill_random(0)
+    e.add_diffuse(0, 0.2)
+    e.prepare(steps, 1)
+    e.run(steps, 1)
+    got = e.download()
+    hist = e.sums_history()
+    info = e.info()
+    e.close()
+    assert info["graph_state"] == 1 and info["graph_launches"] == launches, info
+    want, sums = O.program_step([O.fill_random(H, W)], [(1, 0, 0, 0.2)], steps=steps,
+                                sums_per_step=True)
+    assert np.array_equal(got, want[0])
+    assert hist.shape == (steps, 1)
+    for s, row in enumerate(sums):
+        assert abs(hist[s, 0] - row[0]) <= 1e-12 * abs(row[0]), s
+
+
 C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
             (1, 0, 0, 0.1), (1, 1, 1, 0.1), (1, 2, 2, 0.05), (1, 3, 3, 0.2)]
 
