@@ -108,6 +108,9 @@ namespace {
 #ifndef MM_PROBE_L2ROWS
 #define MM_PROBE_L2ROWS 0  // timing probe (tools/build_variants.sh only): see wave_iter
 #endif
+#ifndef MM_WIDE_ROT
+#define MM_WIDE_ROT 0  // 1 / 2: rotate the wave roles by blockIdx.x (/ 8) mod P (WRot)
+#endif
 #ifndef MM_WIDE_WC
 #define MM_WIDE_WC 1  // column waves per level group (one attribute): WC strips side by side
 #endif                // share one workgroup, their internal edges mended at every hand-off
@@ -890,7 +893,12 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
     __shared__ dv2 lds_g[GL::on ? GL::R * GL::SLOT : 1];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int p = wv / WC, cw = wv % WC;  // level group, column wave
+    // level group, column wave. MM_WIDE_ROT: the roles rotate from workgroup to workgroup,
+    // so the waves of the workgroups sharing a CU that start late (p > 0: the pipeline
+    // fill) or end early (p < P - 1) do not all sit on the same SIMDs
+    const int wr = MM_WIDE_ROT == 0 ? wv
+                   : (wv + WC * (int)((MM_WIDE_ROT == 1 ? blockIdx.x : blockIdx.x / 8) % P)) % (P * WC);
+    const int p = wr / WC, cw = wr % WC;
     long long blk = blockIdx.x;
     if (A.xcd_remap == 1) {
         const long long per = gridDim.x / 8;

@@ -1,5 +1,15 @@
 // mm_wide_k8.hip -- instances of the level-split K-step kernel (mm_wide.hpp) for K = 8:
 // 2 level(s) per wave, 4 waves per workgroup.
+// Tuning (tools/libsweep.py, profiles/r04/k8): barrier groups of 2 rows (2 prefetched):
+// the pipeline fill of the 108-row segments of C2 (4096^2) is 6 iterations shorter per
+// wave, 85.0 / 84.3 vs 87.2 / 86.6 us per 8-step pass in two sweeps; groups of 1 row
+// 101 us; an LDS-DMA input ring 8 / 12 rows deep 86.0 / 86.5 us.
+#ifndef MM_WIDE_U
+#define MM_WIDE_U 2
+#endif
+#ifndef MM_WIDE_B
+#define MM_WIDE_B 2
+#endif
 #include "mm_wide.hpp"
 
 namespace mm {
