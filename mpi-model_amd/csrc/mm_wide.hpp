@@ -103,7 +103,7 @@ namespace {
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
 #ifndef MM_WIDE_GLDS
-#define MM_WIDE_GLDS 0  // R > 0: one attribute, the loading wave streams its input rows through
+#define MM_WIDE_GLDS 0  // R > 2: the loading wave streams its input rows (every attribute) through
 #endif                  // an R-row LDS ring filled by LDS-DMA, R - 1 rows ahead (WGlds)
 #ifndef MM_PROBE_L2ROWS
 #define MM_PROBE_L2ROWS 0  // timing probe (tools/build_variants.sh only): see wave_iter
@@ -153,7 +153,7 @@ struct WXpose {
     static constexpr bool on = C >= 6 && MM_WIDE_XPOSE;
 };
 
-// The loading wave's input ring (MM_WIDE_GLDS = R rows, one attribute): row i of the
+// The loading wave's input ring (MM_WIDE_GLDS = R rows, NA attributes): row i of the
 // segment lands in slot i % R by global_load_lds_dwordx4 (16 B per lane, lane-linear: the
 // ring's row layout [piece][lane] is exactly that), issued R - 1 iterations ahead, so its
 // HBM latency is covered by R - 1 iterations instead of the register prefetch's U, and the
@@ -165,8 +165,9 @@ struct WXpose {
 template <int C, int NA>
 struct WGlds {
     static constexpr int R = MM_WIDE_GLDS;
-    static constexpr bool on = R > 2 && NA == 1 && !WXpose<C>::on;
-    static constexpr int SLOT = (C / 2) * 64;  // dv2 per ring slot
+    static constexpr bool on = R > 2 && !WXpose<C>::on;
+    static constexpr int SLOT = NA * (C / 2) * 64;  // dv2 per ring slot: [attribute][piece][lane]
+    static_assert(!on || (R - 2) * NA * (C / 2) <= 63, "vmcnt counts to 63");
 };
 
 __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
@@ -335,8 +336,8 @@ struct WCtx {
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
     int rdelta;           // WC > 1: dv2 offset of this lane's read (the neighbour wave's row)
-    const double* gsrc;   // WGlds: this lane's column of segment input row 0 (clamped)
-    const dv2* lds_pfr;   // WGlds: the ring (R slots of H2 x 64 dv2)
+    const double* gsrc[NA];  // WGlds: this lane's column of segment input row 0 (clamped)
+    const dv2* lds_pfr;   // WGlds: the ring (R slots of NA x H2 x 64 dv2)
     unsigned pf_lds;      // WGlds: LDS byte address of the ring
     int prow_max;         // WGlds: last segment input row that exists (rB - rA + 2K - 1)
     double* partials;
@@ -562,24 +563,30 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
 #pragma unroll
         for (int h = 0; h < H2; ++h) st.raw[slot][0][h] = load_row(x.in[0], x.xvoff[h] + ro);
     } else if constexpr (ROLE == kRoleFirst && WGlds<C, NA>::on) {
-        // row i is in slot i % R once the DMAs issued after it (rows i+1 .. i+R-2, H2
+        // row i is in slot i % R once the DMAs issued after it (rows i+1 .. i+R-2, NA x H2
         // each) are all that is left in flight; then refill the slot read last iteration
         // with row i + R - 1
         using GL = WGlds<C, NA>;
         constexpr int R = GL::R;
-        wait_vmcnt<(R - 2) * H2>();
+        wait_vmcnt<(R - 2) * NA * H2>();
         const dv2* src = x.lds_pfr + (i % R) * GL::SLOT;
 #pragma unroll
-        for (int h = 0; h < H2; ++h) {
-            const dv2 v = src[64 * h + x.lane];
-            cur[0][2 * h] = v.x;
-            cur[0][2 * h + 1] = v.y;
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h) {
+                const dv2 v = src[64 * (a * H2 + h) + x.lane];
+                cur[a][2 * h] = v.x;
+                cur[a][2 * h + 1] = v.y;
+            }
         }
-        const int nr = min(i + R - 1, x.prow_max);
+        const long long ro = (long long)min(i + R - 1, x.prow_max) * (x.rowb / 8);
         const unsigned slot_b = x.pf_lds + (unsigned)(((i + R - 1) % R) * (GL::SLOT * 16));
 #pragma unroll
-        for (int h = 0; h < H2; ++h)
-            glds16(x.gsrc + (long long)nr * (x.rowb / 8) + 2 * h, slot_b + 1024u * h);
+        for (int a = 0; a < NA; ++a) {
+#pragma unroll
+            for (int h = 0; h < H2; ++h)
+                glds16(x.gsrc[a] + ro + 2 * h, slot_b + 1024u * (a * H2 + h));
+        }
     } else if (kIn) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -761,11 +768,14 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
             using GL = WGlds<C, NA>;
 #pragma unroll
             for (int k = 0; k < GL::R - 1; ++k) {
-                const int nr = min(k, x.prow_max);
+                const long long ro = (long long)min(k, x.prow_max) * (x.rowb / 8);
 #pragma unroll
-                for (int h = 0; h < C / 2; ++h)
-                    glds16(x.gsrc + (long long)nr * (x.rowb / 8) + 2 * h,
-                           x.pf_lds + (unsigned)(k * GL::SLOT * 16 + 1024 * h));
+                for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                    for (int h = 0; h < C / 2; ++h)
+                        glds16(x.gsrc[a] + ro + 2 * h,
+                               x.pf_lds + (unsigned)(k * GL::SLOT * 16 + 1024 * (a * (C / 2) + h)));
+                }
             }
         } else {
 #pragma unroll
@@ -995,7 +1005,8 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
         // holds columns outside the grid, whose cells emit nothing); LDS address = the low
         // 32 bits of the LDS aperture address
         const long long yc = y0 < 0 ? 0 : (y0 > A.pitch - C ? A.pitch - C : y0);
-        x.gsrc = A.in[0] + (long long)(x.rA - K) * A.pitch + yc;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) x.gsrc[a] = A.in[a] + (long long)(x.rA - K) * A.pitch + yc;
         x.lds_pfr = &lds_g[0];
         x.pf_lds = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)&lds_g[0]);
         x.prow_max = x.rB - x.rA + 2 * K - 1;
