@@ -294,7 +294,11 @@ __device__ __forceinline__ void accumc(double& acc, bool row_own, const WLane<C>
 
 // workgroup barrier ordering LDS only: s_waitcnt lgkmcnt(0); s_barrier -- the prefetched
 // HBM rows stay in flight
+#ifndef MM_PROBE_NOBAR
+#define MM_PROBE_NOBAR 0  // timing probe only (wrong results): the row-group barriers dropped
+#endif
 __device__ __forceinline__ void wg_sync() {
+    if (MM_PROBE_NOBAR) return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
