@@ -180,8 +180,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double* first,
                                              rows > 0 ? (int)(rows * pitch * 8) : 0, 0x00020000);
 }
 
+#ifndef MM_LOAD_NT
+#define MM_LOAD_NT 0  // 1: input rows loaded non-temporal (aux nt)
+#endif
 __device__ __forceinline__ dv2 load_row(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MM_LOAD_NT ? 2 : 0));
 }
 
 template <int NT>
