@@ -180,7 +180,9 @@ int mm_device_synchronize(int device);
  * engines accept mm_partition_rows slabs only (floor(H/nranks) rows at least) and
  * return MM_ERR_INVALID otherwise.
  * Environment: MM_PASSK=0 (or MM_FUSE=0) runs one step per kernel pass, MM_GRAPH=0
- * disables the hipGraph replay, MM_WIDE=0/1 selects the level-split K-step kernel for
+ * disables the hipGraph replay (a graph holds MM_GRAPH_MIN_STEPS steps at least and, when
+ * that divides the run, the longest run-dividing block of up to MM_GRAPH_MAX_LAUNCHES step
+ * kernels, default 128), MM_WIDE=0/1 selects the level-split K-step kernel for
  * one-diffusion programs, MM_STEPS_PER_PASS (1..10, or 4/8/12/16/20 with the wide
  * kernel; fixes K), MM_PASS_PLAN=0
  * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
@@ -189,7 +191,7 @@ int mm_device_synchronize(int device);
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
  * path, result unchanged).
  * An RCCL chain runs in lockstep: every rank must call mm_prepare / mm_run with the same
- * step counts and reduce_every, with the same MM_GRAPH setting and the same timing mode
+ * step counts and reduce_every, with the same MM_GRAPH* settings and the same timing mode
  * (mm_set_timing), so that all ranks run the same K-row exchanges and capture the same
  * graphs at the same call (the first capture of each graph agrees on success with one
  * all-reduce, after draining this engine's streams). */
