@@ -186,12 +186,12 @@ def level_row_cycles(cols, n_diffuse=1, n_transfers=0, chain_kernel=0):
     """VALU cycles one wave issues per level-row of its strip: per diffusing
     attribute 7 fp64 instructions per column of a lane (4 cycles each on a SIMD) and the
     two fp64 DPP neighbour moves (4 v_mov_dpp, 2 cycles each); per transfer of a chain and
-    column, 3 fp64 instructions (out = r*u_a, u_a - out, u_b + out), plus with run-time
-    operands (chain_kernel 1: register-vector indexing) two v_mov_b32 per access of u_a /
-    u_b read and written (8 per transfer and column, 2 cycles each)."""
+    column, 3 fp64 instructions (out = r*u_a, u_a - out, u_b + out) -- with compile-time
+    operands (mm.MM_CHAIN_RING) and with chain_asm's run-time operands (mm.MM_CHAIN_RUNTIME)
+    alike: chain_asm indexes the fp64 instructions' own operands, no moves."""
+    del chain_kernel  # both chain kernels issue the same instructions per transfer
     diff = n_diffuse * (7 * cols * 4 + 4 * 2)
-    per_transfer = 3 * 4 + (8 * 2 if chain_kernel == 1 else 0)  # 2 ring, 3 chain_asm: none
-    return diff + n_transfers * cols * per_transfer
+    return diff + n_transfers * cols * 3 * 4
 
 
 def valu_roof(passes, h, W, kern_avg_ms, lr_cycles=None):

@@ -101,11 +101,18 @@ typedef struct mm_info {
     long long hist_entries;    /* step-sum history entries enqueued (MPI_Report) */
     char graph_note[160];      /* why capture was refused ("" otherwise) */
     int seg_waves_per_cu;      /* resident waves per CU the K-step segment plan assumes */
-    int chain_kernel;          /* transfer chains of a four-attribute mm_wide_kernel pass:
-                                  0 none / not that kernel, 1 generic (operands picked at
-                                  run time), 2 the ring t -> t+1 mod 4 with compile-time
-                                  operands */
+    int chain_kernel;          /* transfer chains of a four-attribute mm_wide_kernel pass
+                                  (MM_CHAIN_*): MM_CHAIN_NONE not that kernel,
+                                  MM_CHAIN_RING the ring t -> t+1 mod 4 with compile-time
+                                  operands, MM_CHAIN_RUNTIME any chain, its operands
+                                  indexed at run time in the register file (chain_asm);
+                                  the value 1 is not used */
 } mm_info;
+
+/* mm_info.chain_kernel */
+#define MM_CHAIN_NONE 0
+#define MM_CHAIN_RING 2
+#define MM_CHAIN_RUNTIME 3
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
 int mm_abi_version(void);
@@ -186,8 +193,12 @@ int mm_device_synchronize(int device);
  * one-diffusion programs, MM_STEPS_PER_PASS (1..10, or 4/8/12/16/20 with the wide
  * kernel; fixes K), MM_PASS_PLAN=0
  * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
- * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal policy)
- * override tuning; MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
+ * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal stores;
+ * the four-attribute K = 8 instances always store non-temporal) override tuning; MM_LIN=0/1
+ * turns the wide kernel's linear plan (one round of workgroups sharing a pass; auto on
+ * one-attribute passes with >= 24 K rows per workgroup, not with MM_SEG_WAVES) off / on,
+ * MM_LIN_WORKERS / MM_LIN_MAXR set its workgroups / segment length (tests);
+ * MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
  * path, result unchanged).
  * An RCCL chain runs in lockstep: every rank must call mm_prepare / mm_run with the same

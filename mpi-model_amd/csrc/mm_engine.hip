@@ -76,10 +76,6 @@ struct FlowDesc {
     double rate;
 };
 
-// mm_wide_kernel block order: runs of kXcdChunk side-by-side strips per XCD (0: plain
-// round-robin); see wide_grid in mm_wide.hpp
-constexpr int kXcdChunk = 0;
-
 }  // namespace
 
 struct mm_engine {
@@ -112,8 +108,10 @@ struct mm_engine {
     bool plan = true;        // pass-length planner (MM_PASS_PLAN=0: balanced passes of K)
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
     double seg_edge = 0.0;   // edge-strip segment length / interior length (MM_SEG_EDGE; 0: auto)
-    int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP)
-    int xcd_chunk = kXcdChunk;  // mm_wide_kernel: runs of this many strips per XCD (MM_XCD_CHUNK, 0: off)
+    int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP, mm_passk_kernel)
+    int lin = -1;            // mm_wide_kernel linear plan (MM_LIN=0/1; -1 auto, wide_lin)
+    int lin_workers = 0;     // linear plan: workgroups (MM_LIN_WORKERS; 0: the resident slots)
+    int lin_maxr = 0;        // linear plan: rows per segment at most (MM_LIN_MAXR; 0: offset bound)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
     std::map<long long, int> bpc;  // wide kernel blocks/CU cache: (variant, red, k)
@@ -565,12 +563,61 @@ long long nstrips_wide(const mm_engine* e, int k) {
     return (e->d.W + oc - 1) / oc;
 }
 
+// Linear plan of rows [lo, hi) for the wide kernel (mm_wide.hpp lin_cost): one round of
+// workgroups, as many as the chip holds at once (the kernel's blocks per CU x CUs), each
+// taking an equal share of the range's cost -- its rows in one strip or the tail of one and
+// the head of the next -- with the edge strips' rows at 1 / seg_edge the cost of the
+// others'. Auto (MM_LIN unset, no MM_SEG_WAVES): one attribute, at least 24 K rows per workgroup, so the
+// pipeline fill of a workgroup's (at most two, plus offset-bound splits) segments stays
+// small against its rows. Returns false where the segment plan runs instead.
+bool wide_lin(mm_engine* e, int k, long long slots, double edge, mm::PassArgs& A,
+              long long lo, long long hi) {
+    const long long n = hi - lo, ns = A.nstrips;
+    if (e->lin == 0 || n <= 0 || ns <= 0) return false;
+    const int e2 = std::max(2, (int)std::lround(2.0 / edge));
+    const double rows_eq = (double)n * (ns >= 2 ? (double)(ns - 2) + e2 / 2.0 : e2 / 2.0);
+    long long workers = e->lin_workers > 0 ? e->lin_workers : slots;
+    if (e->lin < 0) {
+        if (e->seg_waves > 0.0 || e->na != 1 || rows_eq / (double)slots < 24.0 * k) return false;
+    } else if (e->lin_workers <= 0) {
+        // forced on a small range: a workgroup per 3K rows at least
+        workers = std::min<long long>(slots, std::max<long long>(1, (long long)(rows_eq / (3.0 * k))));
+    }
+    workers = std::max<long long>(1, std::min<long long>(workers, n * ns));
+    const long long maxr = std::max<long long>(1, mm::passk_max_rows(k, e->pitch));
+    A.seg = 1;
+    A.lin = 1;
+    A.lin_e2 = e2;
+    A.lin_maxr = (int)(e->lin_maxr > 0 ? std::min<long long>(e->lin_maxr, maxr) : maxr);
+    A.ra0 = (int)lo;
+    A.ra1 = (int)hi;
+    // every workgroup's segments fit the kernel's list (kLinSegs): more workgroups while
+    // one does not (a range shorter than a workgroup's share of rows, or short MM_LIN_MAXR)
+    for (;;) {
+        A.waves_total = workers;
+        int most = 0;
+        for (long long b = 0; b < workers; ++b)
+            most = std::max(most, mm::lin_segments(A, b, nullptr, 0));
+        if (most <= mm::kLinSegs) break;
+        if (workers >= n * ns) {
+            A.lin = 0;
+            return false;
+        }
+        workers = std::min(n * ns, workers * 2);
+    }
+    A.th = (int)std::max<long long>(1, (long long)(rows_eq / (double)workers));  // rows per workgroup (info)
+    A.th_edge = A.th;
+    A.rb0 = A.rb1 = 0;
+    A.waves_a = A.waves_total = workers;
+    return true;
+}
+
 // Segment plan of rows [lo, hi) for the wide kernel: one workgroup per strip segment, r
 // rows per interior-strip segment and re per edge-strip segment, the smallest r for which
 // the blocks fit seg_waves x the chip's resident blocks. Auto: 4 per resident slot, halved
 // (down to 1) while segments are shorter than 24 K rows -- a segment pays 3K - 1 pipeline
 // iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
-// profiles/r03/kernel_table).
+// profiles/r03/kernel_table). Large ranges take the linear plan instead (wide_lin).
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
     const int nt = (e->variant & 1) | wvar(e);
     const int c = wcols(e, k);
@@ -579,6 +626,8 @@ void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lo
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
+    A.lin = 0;
+    if (wide_lin(e, k, (long long)e->ncu * bpc, edge, A, lo, hi)) return;
     const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
     auto re_of = [&](long long rr) {
         return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
@@ -620,15 +669,13 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     fill_args(e, e->passes[0], A);
     const int perm = relabel(e, A);
     A.nstrips = (int)nstrips_wide(e, k);
-    A.xcd_remap = e->xcd ? e->xcd : e->xcd_chunk;  // MM_XCD_REMAP=1, else XCD chunks
-    long long total_blocks = 0;  // partials units: blocks x column waves
-    const int wc = mm::wide_wc(k, wcols(e, k), e->na);
+    long long total_blocks = 0;  // partials units: one per workgroup
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(split_begin(e, depth));
         wide_range(e, k, red, A, depth, h - depth);
-        const long long interior = A.waves_total * wc;
+        const long long interior = A.waves_total;
         mm::PassArgs B = A;
-        B.xcd_remap = 0;
+        B.lin = 0;
         B.th = B.th_edge = depth;
         B.ra0 = 0;
         B.ra1 = depth;
@@ -642,14 +689,14 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         e->comm_live = true;
         A.partial_base = 0;
         MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
-        total_blocks = interior + B.waves_total * wc;
+        total_blocks = interior + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
         if (e->split) MM_TRY(unsplit_halo(e, depth));
         wide_range(e, k, red, A, 0, h);
         A.partial_base = 0;
         MM_TRY(launch_timed(e, red, A, h, time_it, -k));
-        total_blocks = A.waves_total * wc;
+        total_blocks = A.waves_total;
     }
     if (red)
         MM_HIP(mm::launch_finalize_levels(e->partials, total_blocks, k, e->na, mask, e->hist,
@@ -1142,7 +1189,9 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
-    if (const char* c = std::getenv("MM_XCD_CHUNK")) e->xcd_chunk = std::max(0, std::atoi(c)) == 1 ? 2 : std::max(0, std::atoi(c));
+    if (const char* l = std::getenv("MM_LIN")) e->lin = std::atoi(l) != 0 ? 1 : 0;
+    if (const char* l = std::getenv("MM_LIN_WORKERS")) e->lin_workers = std::max(0, std::atoi(l));
+    if (const char* l = std::getenv("MM_LIN_MAXR")) e->lin_maxr = std::max(0, std::atoi(l));
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
         if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4, 1) || mm::wide_has(v, 2, 4)))))
@@ -1299,7 +1348,7 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
         const int c = wcols(e, spl);
         info->waves_per_pass = A.waves_total * mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
         info->kernel = 3;
-        if (e->na > 1) info->chain_kernel = (wring(e) && spl == 8) ? 2 : 3;
+        if (e->na > 1) info->chain_kernel = (wring(e) && spl == 8) ? MM_CHAIN_RING : MM_CHAIN_RUNTIME;
         info->seg_waves_per_cu =
             e->bpc[((long long)((e->variant & 1) | wvar(e)) << 8) | spl] *
             mm::wide_waves_per_block(spl, c, e->na, wring(e) != 0);
@@ -1555,7 +1604,7 @@ int mm_pass_kernel(mm_engine* e, int k, int* kernel, int* cols_per_lane, long lo
     } else if (use_wide(e, k)) {
         *kernel = 3;
         *cols_per_lane = wcols(e, k);
-        *strips = nstrips_wide(e, k) * mm::wide_wc(k, wcols(e, k), e->na);  // 64-lane columns
+        *strips = nstrips_wide(e, k);
     } else {
         *kernel = 2;
         *cols_per_lane = 2;

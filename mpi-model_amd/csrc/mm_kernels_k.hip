@@ -111,32 +111,18 @@ bool wide_has(int k, int c, int na) {
     return c == 4 && (k == 4 || k == 8 || k == 12 || k == 16 || k == 20);
 }
 
-int wide_wc(int k, int c, int na) {
-    if (!wide_has(k, c, na) || na > 1) return 1;
-    switch (k) {
-        case 4: return wide_wc_k4();
-        case 8: return wide_wc_k8();
-        case 12: return wide_wc_k12();
-        case 16: return wide_wc_k16();
-        default: return wide_wc_k20();
-    }
-}
-
 int wide_out_cols(int k, int c, int na) {
-    // WCols of the instance: one attribute runs K / 4 levels per wave (4 level groups)
-    const int wc = wide_wc(k, c, na);
-    const int lh = (k + c - 1) / c, kw = na > 1 ? 2 : k / 4;
-    const int lhw = wc > 1 ? (kw + c - 1) / c : 0;
-    return c * (64 - 2 * lhw) * (wc - 1) + 64 * c - 2 * c * lh;
+    (void)na;
+    return 64 * c - 2 * c * ((k + c - 1) / c);  // 64 lanes less ceil(K / C) halo lanes a side
 }
 
 int wide_waves_per_block(int k, int c, int na, bool ring) {
     if (!wide_has(k, c, na)) return 0;
     if (na > 1 && k == 8 && ring) return widear_waves_k8();
     if (na == 1 && k == 20) return wide_waves_k20();  // MM_K20_KW levels per wave
-    // one attribute: K / 4 levels per wave, 4 level groups x wide_wc column waves; four
-    // attributes: mm_widea_k4 1 level per wave, mm_widea_k8 2
-    return 4 * wide_wc(k, c, na);
+    // one attribute: K / 4 levels per wave, 4 level groups; four attributes: mm_widea_k4
+    // 1 level per wave, mm_widea_k8 2
+    return 4;
 }
 
 namespace {

@@ -23,12 +23,8 @@
 // diffusions) hold NA windows per level: C = 2 columns per lane keeps the state of a level
 // near a one-attribute level's at C = 4 (NA * C doubles per cell row).
 //
-// C = 8 columns per lane (KW <= 3 levels at <= 256 VGPRs: gfx950's arch VGPRs stop at 256
-// per wave, the rest of the 512-entry file is AGPRs that VALU operations cannot read) was
-// built and measured at 2.5x the time of C = 4 whether its levels were ordered with the
-// pend hand-off or ascending, and 1.75x with deeper prefetch at one workgroup per CU
-// (profiles/r03/r3d, profiles/r03/var). Not diagnosed further (a suspect: with a 64-B slice
-// per lane every 16-B load instruction touches 64 lines a quarter each); not instantiated.
+// C = 8 columns per lane, column waves, an LDS-DMA input ring, role rotation and
+// non-temporal loads were built, measured and dropped (git history).
 //
 // Pipeline (the skew of mm_passk.hpp, across waves): level j's m-th input row arrives at
 // iteration m + 3(j-1) and it emits one row per input from its third input on; level j's
@@ -53,8 +49,7 @@ namespace mm {
 // per-K entry points (mm_wide_k*.hip: one attribute, C = 4)
 #define MM_WIDE_DECL(K)                                                                    \
     hipError_t wide_launch_k##K(bool red, const PassArgs& a, hipStream_t s, int v);       \
-    int wide_blocks_k##K(bool red, int nt);                                                \
-    int wide_wc_k##K();
+    int wide_blocks_k##K(bool red, int nt);
 MM_WIDE_DECL(4)
 MM_WIDE_DECL(8)
 MM_WIDE_DECL(12)
@@ -93,100 +88,18 @@ namespace {
 #ifndef MM_WIDE_B
 #define MM_WIDE_B 4  // rows per barrier group
 #endif
-#ifndef MM_WIDE_LEVEL_BARRIER
-#define MM_WIDE_LEVEL_BARRIER 0  // scheduling barrier after every this many levels (0: none)
-#endif
 #ifndef MM_WIDE_MIN_WAVES
 #define MM_WIDE_MIN_WAVES 2  // __launch_bounds__ waves per SIMD of the C = 4 instances
 #endif
 #ifndef MM_WIDE_ASC
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
-#ifndef MM_WIDE_GLDS
-#define MM_WIDE_GLDS 0  // R > 2: the loading wave streams its input rows (every attribute) through
-#endif                  // an R-row LDS ring filled by LDS-DMA, R - 1 rows ahead (WGlds)
-#ifndef MM_PROBE_L2ROWS
-#define MM_PROBE_L2ROWS 0  // timing probe (tools/build_variants.sh only): see wave_iter
-#endif
-#ifndef MM_WIDE_ROT
-#define MM_WIDE_ROT 0  // 1 / 2: rotate the wave roles by blockIdx.x (/ 8) mod P (WRot)
-#endif
-#ifndef MM_WIDE_WC
-#define MM_WIDE_WC 1  // column waves per level group (one attribute): WC strips side by side
-#endif                // share one workgroup, their internal edges mended at every hand-off
-
-// Column waves (MM_WIDE_WC = WC > 1). A workgroup holds WC waves per level group, side by
-// side: wave (p, c) loads / computes the 64*C columns from its span's first column +
-// c * WSTEP. Inside a wave the DPP neighbour of its edge lanes is 0, so after the KW levels
-// of a group its LHW = ceil(KW / C) edge lanes next to another column wave are spoiled --
-// the overlap of 2 * LHW lanes between neighbours covers them: at the LDS hand-off a wave
-// of the next group reads those lanes from its neighbour's row instead (WCtx::rdelta).
-// Only the span's two outer edges lose K columns to the halo, so a workgroup outputs
-// WSTEP * (WC - 1) + 64C - 2C * LH columns (WC = 2, K = 20: 456 of 512 loaded = 89 %,
-// against 216 of 256 = 84 % for one wave per group).
-template <int C, int KW, int K, int WC>
-struct WCols {
-    static constexpr int LH = (K + C - 1) / C;                   // outer halo lanes per side
-    static constexpr int LHW = WC > 1 ? (KW + C - 1) / C : 0;    // spoiled lanes per inner edge
-    static constexpr int WSTEP = C * (64 - 2 * LHW);             // columns between column waves
-    static constexpr int OC = WSTEP * (WC - 1) + 64 * C - 2 * C * LH;  // output columns
-};
 
 // Iterations between two consecutive levels' first inputs: 3 with the pend hand-off (level
 // q+1 takes level q's row of the previous iteration: the KW level chains of one iteration
 // are independent), 2 with MM_WIDE_ASC (level q+1 takes it in the same iteration: C
 // registers per level fewer, the scheduler interleaves consecutive iterations instead).
 constexpr int kSkew = MM_WIDE_ASC ? 2 : 3;
-
-#ifndef MM_WIDE_XPOSE
-#define MM_WIDE_XPOSE 1  // C = 8: rows in / out of HBM coalesced, transposed through LDS
-#endif
-
-// With 8 columns per lane a lane's slice of a row is 64 B: loaded / stored in place, each
-// 16-B wave-instruction touches 64 separate 64-B segments and the texture addresser
-// becomes the bottleneck (profiles/r03/w8probe: 2.9x its busy cycles for the same bytes).
-// XPOSE moves rows piece-major instead -- piece h of lane l = columns c0 + 128h + 2l, +1,
-// 1 KiB contiguous per instruction -- and transposes them through a 4-KiB LDS scratch of
-// the first (input) and the last (output) wave.
-template <int C>
-struct WXpose {
-    static constexpr bool on = C >= 6 && MM_WIDE_XPOSE;
-};
-
-// The loading wave's input ring (MM_WIDE_GLDS = R rows, NA attributes): row i of the
-// segment lands in slot i % R by global_load_lds_dwordx4 (16 B per lane, lane-linear: the
-// ring's row layout [piece][lane] is exactly that), issued R - 1 iterations ahead, so its
-// HBM latency is covered by R - 1 iterations instead of the register prefetch's U, and the
-// U prefetch registers are free. The DMAs are inline asm, outside the compiler's s_waitcnt
-// bookkeeping: the wave counts them itself (vmcnt) before it reads a slot, and it issues
-// no other vector-memory loads in its loop. Addresses have no range check (buffer loads
-// had): rows are clamped to the segment's [rA - K, rB + K), columns outside the pitch to
-// the row's first / last piece -- columns outside the grid emit nothing either way.
-template <int C, int NA>
-struct WGlds {
-    static constexpr int R = MM_WIDE_GLDS;
-    static constexpr bool on = R > 2 && !WXpose<C>::on;
-    static constexpr int SLOT = NA * (C / 2) * 64;  // dv2 per ring slot: [attribute][piece][lane]
-    static_assert(!on || (R - 2) * NA * (C / 2) <= 63, "vmcnt counts to 63");
-};
-
-__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 enum { kBodyFast = 0, kBodyEdge = 1, kBodyGen = 2 };
 
@@ -294,11 +207,7 @@ __device__ __forceinline__ void accumc(double& acc, bool row_own, const WLane<C>
 
 // workgroup barrier ordering LDS only: s_waitcnt lgkmcnt(0); s_barrier -- the prefetched
 // HBM rows stay in flight
-#ifndef MM_PROBE_NOBAR
-#define MM_PROBE_NOBAR 0  // timing probe only (wrong results): the row-group barriers dropped
-#endif
 __device__ __forceinline__ void wg_sync() {
-    if (MM_PROBE_NOBAR) return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -334,18 +243,9 @@ struct WCtx {
     long long g0;         // global row of input row 0 (rA - K)
     double r[NA], r8[NA];
     unsigned voff, soff, rowb;
-    unsigned xvoff[C / 2], xsoff[C / 2];  // WXpose: per-piece load / store offsets
-    dv2* lds_x;                           // WXpose: this wave's transpose scratch
     __amdgpu_buffer_rsrc_t in[NA], out[NA];
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
-    int rdelta;           // WC > 1: dv2 offset of this lane's read (the neighbour wave's row)
-    const double* gsrc[NA];  // WGlds: this lane's column of segment input row 0 (clamped)
-    const dv2* lds_pfr;   // WGlds: the ring (R slots of NA x H2 x 64 dv2)
-    unsigned pf_lds;      // WGlds: LDS byte address of the ring
-    int prow_max;         // WGlds: last segment input row that exists (rB - rA + 2K - 1)
-    double* partials;
-    long long pbase;
     const PassArgs* A;    // transfer chains (NA > 1)
     // MM_CHAIN_ASM: register offsets of the pre / post chains' operands (chain_asm)
     int pia[kMaxChain], pib[kMaxChain], qia[kMaxChain], qib[kMaxChain];
@@ -472,9 +372,10 @@ __device__ __forceinline__ void chain_cols(double (&u)[NA][C], int n, const sign
 #endif
 }
 
-// The pass's pre-chain on a level's input row (NA > 1): MM_CHAIN_ASM always runs its four
-// slots (no branch in the loop body; unused slots act on the pad), the other instances
-// only when the pass has one.
+// The pass's pre-chain on a level's input row (NA > 1): MM_CHAIN_ASM runs the chain's
+// first npre slots and leaves the asm block through a scalar branch after the last one
+// (one straight-line block for the compiler; a transfer whose outflow leaves the system
+// adds it to the pad pair), the other instances only when the pass has a pre-chain.
 template <int C, int NA>
 __device__ __forceinline__ void pre_chain(const WCtx<C, NA>& x, double (&u)[NA][C]) {
     if constexpr (NA > 1 && MM_CHAIN_ASM) {
@@ -551,47 +452,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;   // input from HBM
     constexpr bool kOut = ROLE == kRoleLast || ROLE == kRoleOnly;  // output to HBM
     double cur[NA][C];  // the row level q consumes
-    if constexpr (kIn && WXpose<C>::on) {
-        // the prefetched row is piece-major: through the scratch into this lane's columns
-        static_assert(NA == 1, "one attribute");
-#pragma unroll
-        for (int h = 0; h < H2; ++h) x.lds_x[64 * h + x.lane] = st.raw[slot][0][h];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int h = 0; h < H2; ++h) {
-            const dv2 v = x.lds_x[H2 * x.lane + h];
-            cur[0][2 * h] = v.x;
-            cur[0][2 * h + 1] = v.y;
-        }
-        const unsigned ro = (unsigned)(i + U) * x.rowb;
-#pragma unroll
-        for (int h = 0; h < H2; ++h) st.raw[slot][0][h] = load_row(x.in[0], x.xvoff[h] + ro);
-    } else if constexpr (ROLE == kRoleFirst && WGlds<C, NA>::on) {
-        // row i is in slot i % R once the DMAs issued after it (rows i+1 .. i+R-2, NA x H2
-        // each) are all that is left in flight; then refill the slot read last iteration
-        // with row i + R - 1
-        using GL = WGlds<C, NA>;
-        constexpr int R = GL::R;
-        wait_vmcnt<(R - 2) * NA * H2>();
-        const dv2* src = x.lds_pfr + (i % R) * GL::SLOT;
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-#pragma unroll
-            for (int h = 0; h < H2; ++h) {
-                const dv2 v = src[64 * (a * H2 + h) + x.lane];
-                cur[a][2 * h] = v.x;
-                cur[a][2 * h + 1] = v.y;
-            }
-        }
-        const long long ro = (long long)min(i + R - 1, x.prow_max) * (x.rowb / 8);
-        const unsigned slot_b = x.pf_lds + (unsigned)(((i + R - 1) % R) * (GL::SLOT * 16));
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-#pragma unroll
-            for (int h = 0; h < H2; ++h)
-                glds16(x.gsrc[a] + ro + 2 * h, slot_b + 1024u * (a * H2 + h));
-        }
-    } else if (kIn) {
+    if (kIn) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
@@ -605,13 +466,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
 #endif
             }
         }
-#if MM_PROBE_L2ROWS
-        // timing probe only (wrong results): the loading wave re-reads the segment's first
-        // 8 rows, L2-resident, instead of streaming -- what HBM latency costs the pass
-        const unsigned o = x.voff + (unsigned)((i + U) & 7) * x.rowb;
-#else
         const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;
-#endif
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
@@ -623,7 +478,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
             for (int h = 0; h < H2; ++h) {
-                const dv2 v = src[64 * (a * H2 + h) + x.lane + x.rdelta];
+                const dv2 v = src[64 * (a * H2 + h) + x.lane];
                 cur[a][2 * h] = v.x;
                 cur[a][2 * h + 1] = v.y;
             }
@@ -675,22 +530,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
             }
         }
         if (q == KW - 1) {
-            if constexpr (kOut && WXpose<C>::on) {  // level K: output row m - 2, piece-major
-                const unsigned ro = (unsigned)(m - 2) * x.rowb;
-#pragma unroll
-                for (int h = 0; h < H2; ++h) {
-                    dv2 v;
-                    v.x = o[0][2 * h];
-                    v.y = o[0][2 * h + 1];
-                    x.lds_x[H2 * x.lane + h] = v;
-                }
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int h = 0; h < H2; ++h) {
-                    const dv2 v = x.lds_x[64 * h + x.lane];
-                    store_row<NT>(x.out[0], x.xsoff[h] + ro, v.x, v.y);
-                }
-            } else if (kOut) {  // level K: output row m - 2 of the segment
+            if (kOut) {  // level K: output row m - 2 of the segment
                 const unsigned so = x.soff + (unsigned)(m - 2) * x.rowb;
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
@@ -723,10 +563,6 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
                 }
             }
         }
-#if MM_WIDE_LEVEL_BARRIER
-        // at most MM_WIDE_LEVEL_BARRIER levels in flight: bounds the live registers
-        if (qq + 1 < KW && (qq + 1) % MM_WIDE_LEVEL_BARRIER == 0) __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 }
 
@@ -752,8 +588,11 @@ __device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, 
 }
 
 // The whole schedule of one wave. MID: body of the groups whose rows are all interior.
+// RED: every level's sum of this wave's owned cells is added to carry[level][attribute]
+// (wave-uniform), so a workgroup that runs several segments sums them all.
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
-__device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, int iend) {
+__device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
+                                         double (&carry)[KW][NA]) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     static_assert(B % U == 0, "ring slots repeat within a group");
@@ -768,31 +607,14 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
     if (kIn) {
         // start = 0: the prologue and the iterations up to the first group boundary are
         // unrolled (compile-time ring slots)
-        if constexpr (ROLE == kRoleFirst && WGlds<C, NA>::on) {  // rows 0 .. R-2 of the ring
-            using GL = WGlds<C, NA>;
-#pragma unroll
-            for (int k = 0; k < GL::R - 1; ++k) {
-                const long long ro = (long long)min(k, x.prow_max) * (x.rowb / 8);
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-#pragma unroll
-                    for (int h = 0; h < C / 2; ++h)
-                        glds16(x.gsrc[a] + ro + 2 * h,
-                               x.pf_lds + (unsigned)(k * GL::SLOT * 16 + 1024 * (a * (C / 2) + h)));
-                }
-            }
-        } else {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
 #pragma unroll
                 for (int h = 0; h < C / 2; ++h)
-                    st.raw[k][a][h] = WXpose<C>::on
-                                          ? load_row(x.in[a], x.xvoff[h] + k * x.rowb)
-                                          : load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
+                    st.raw[k][a][h] = load_row(x.in[a], x.voff + 16 * h + k * x.rowb);
             }
-        }
         }
 #pragma unroll
         for (int t = 0; t < G::T0; ++t) {
@@ -842,130 +664,53 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, long long wid, in
         wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
     }
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
-    if (RED) {  // partials[partial_base + unit][K][NA], unit = block * WC + c: this wave's KW levels
+    if (RED) {
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
 #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                const double v = wave_sum_k(st.acc[q][a]);
-                if (x.lane == 0) x.partials[((x.pbase + wid) * K + x.p * KW + q) * NA + a] = v;
-            }
+            for (int a = 0; a < NA; ++a) carry[q][a] = carry[q][a] + wave_sum_k(st.acc[q][a]);
         }
     }
 }
 
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int MID>
-__device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, long long wid, int iend) {
+__device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, int iend,
+                                              double (&carry)[KW][NA]) {
     if (P == 1)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleOnly, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleOnly, MID>(x, iend, carry);
     else if (x.p == 0)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleFirst, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleFirst, MID>(x, iend, carry);
     else if (x.p == P - 1)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleLast, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleLast, MID>(x, iend, carry);
     else
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID>(x, wid, iend);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID>(x, iend, carry);
 }
 
-// Edge-strip blocks of range a (seg_map puts them first), rounded up to a multiple of 8.
-__host__ __device__ inline long long wide_edge_blocks8(const PassArgs& A) {
-    const long long n = A.ra1 - A.ra0;
-    const long long e = A.nstrips < 3 || n <= 0 ? 0 : 2 * ((n + A.th_edge - 1) / A.th_edge);
-    return (e + 7) / 8 * 8;
-}
-
-// Grid of a launch: waves_total blocks, padded for the XCD orders (the padding blocks
-// map past waves_total and exit at once).
-__host__ __device__ inline long long wide_grid(const PassArgs& A) {
-    const long long t = A.waves_total;
-    if (A.xcd_remap == 1) return (t + 7) / 8 * 8;
-    if (A.xcd_remap > 1) {
-        const long long e8 = wide_edge_blocks8(A), q = 8LL * A.xcd_remap;
-        return t <= e8 ? e8 : e8 + (t - e8 + q - 1) / q * q;
-    }
-    return t;
-}
-
-// K = KW * P fused steps per launch of an NA-attribute one-pass program (NA = 1: one
-// diffusion; NA > 1: pre-chain, diffusions of the attributes in diffuse_mask, post-chain),
-// one workgroup (P waves) per strip segment, C columns per lane, MW waves per SIMD. The
-// segment map is mm_passk.hpp's seg_map with blocks in place of waves: the two edge strips
-// first (A.th_edge rows), then the others (A.th rows). RED: every level's sums of the
-// block's output cells into partials[partial_base + block * WC + column wave][K][NA]. NT & 1:
-// non-temporal stores. MM_WIDE_WC column waves per level group (WCols).
-template <int C, int NA, int KW, int P, int MW, int U, int B, bool RED, int NT>
-__global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const PassArgs A) {
+// One strip segment [rA, rB) (local rows) of strip `strip`: this wave's part of it (level
+// group p), carrying the level sums (RED). Every wave of the workgroup passes the same
+// barriers and ends with one, so the LDS ring is free for the next segment.
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT>
+__device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p, int lane,
+                                             int strip, int rA, int rB,
+                                             double (&carry)[KW][NA]) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
-    constexpr int WC = MM_WIDE_WC;
-    using WL = WCols<C, KW, K, WC>;
-    constexpr int LH = WL::LH;  // halo lanes per side
-    constexpr int OC = WL::OC;  // output columns per strip
-    constexpr int RW = 32 * C * NA;  // dv2 per LDS row
-    __shared__ dv2 lds[P > 1 ? P - 1 : 1][WC][G::RL][RW];
-    __shared__ dv2 lds_x[WXpose<C>::on ? 2 : 1][WXpose<C>::on ? 32 * C : 1];
-    using GL = WGlds<C, NA>;
-    __shared__ dv2 lds_g[GL::on ? GL::R * GL::SLOT : 1];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // level group, column wave. MM_WIDE_ROT: the roles rotate from workgroup to workgroup,
-    // so the waves of the workgroups sharing a CU that start late (p > 0: the pipeline
-    // fill) or end early (p < P - 1) do not all sit on the same SIMDs
-    const int wr = MM_WIDE_ROT == 0 ? wv
-                   : (wv + WC * (int)((MM_WIDE_ROT == 1 ? blockIdx.x : blockIdx.x / 8) % P)) % (P * WC);
-    const int p = wr / WC, cw = wr % WC;
-    long long blk = blockIdx.x;
-    if (A.xcd_remap == 1) {
-        const long long per = gridDim.x / 8;
-        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    } else if (A.xcd_remap > 1) {
-        // XCD chunks (wide_grid): hardware block b runs on XCD b % 8. The first e8 blocks
-        // (the two edge strips' segments, rounded up to 8) keep that round-robin order, so
-        // the slow edge blocks spread over all XCDs; after them each XCD takes runs of
-        // S = xcd_remap consecutive logical blocks -- side-by-side strips of one row
-        // segment, whose 2K overlapping columns its L2 then serves once
-        const long long e8 = wide_edge_blocks8(A);
-        if (blk >= e8) {
-            const long long S = A.xcd_remap, r = blk - e8, j = r / 8;
-            blk = e8 + (j / S) * 8 * S + (r % 8) * S + j % S;
-        }
-    }
-    if (blk >= A.waves_total) return;  // the whole block: no barrier is left waiting
-
-    int rlo, rhi;
-    long long w = blk;
-    if (w < A.waves_a) {
-        rlo = A.ra0;
-        rhi = A.ra1;
-    } else {
-        w -= A.waves_a;
-        rlo = A.rb0;
-        rhi = A.rb1;
-    }
+    constexpr int LH = (K + C - 1) / C;       // halo lanes per side
+    constexpr int OC = 64 * C - 2 * C * LH;   // output columns per strip
+    constexpr int RW = 32 * C * NA;           // dv2 per LDS row
     WCtx<C, NA> x;
-    int strip;
-    seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, strip, x.rA, x.rB);
+    x.rA = rA;
+    x.rB = rB;
     const long long W = A.W;
-    // first loaded column of this wave: the strip's span starts C * LH columns before its
-    // first output column, column wave cw WSTEP columns further per wave
-    const long long c0 = (long long)strip * OC - C * LH + (long long)cw * WL::WSTEP;
+    // first loaded column: the strip's span starts C * LH columns before its first output
+    // column
+    const long long c0 = (long long)strip * OC - C * LH;
     const long long y0 = c0 + C * lane;
     const bool in_row = y0 >= 0 && y0 < A.pitch;  // y0 % C == 0, pitch % 128 == 0
-    // output lanes: inside the outer halo, and at an inner edge up to the neighbour's
-    const int slo = cw == 0 ? LH : WL::LHW, shi = cw == WC - 1 ? 64 - LH : 64 - WL::LHW;
-    const bool store_lane = lane >= slo && lane < shi && y0 < W;
+    const bool store_lane = lane >= LH && lane < 64 - LH && y0 < W;
     x.voff = in_row ? (unsigned)(y0 * 8) : kOOBk;
     // columns past W inside the pitch are padding: writing them is harmless
     x.soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
-    if (WXpose<C>::on) {  // piece h of lane l: columns c0 + 128h + 2l, +1
-#pragma unroll
-        for (int h = 0; h < C / 2; ++h) {
-            const long long yc = c0 + 128LL * h + 2 * lane;
-            x.xvoff[h] = yc >= 0 && yc < A.pitch ? (unsigned)(yc * 8) : kOOBk;
-            const bool st_ok = yc >= c0 + C * LH && yc < c0 + 64 * C - C * LH && yc < W;
-            x.xsoff[h] = st_ok ? (unsigned)(yc * 8) : kOOBk;
-        }
-        x.lds_x = &lds_x[p == 0 ? 0 : (WXpose<C>::on ? 1 : 0)][0];
-    }
     x.rowb = (unsigned)(A.pitch * 8);
     x.c.H = A.H;
     x.c.special = false;
@@ -993,30 +738,8 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
                             A.pitch);
         x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
     }
-    x.lds_in = p > 0 ? &lds[p - 1][cw][0][0] : &lds[0][0][0][0];
-    x.lds_out = p < P - 1 ? &lds[p][cw][0][0] : &lds[0][0][0][0];
-    // inner-edge lanes read the row the neighbouring column wave wrote (same slot and
-    // piece, 64 - 2 LHW lanes over, one region of RL rows further / back)
-    x.rdelta = 0;
-    if (WC > 1 && p > 0) {
-        if (cw > 0 && lane < WL::LHW)
-            x.rdelta = -G::RL * RW + (64 - 2 * WL::LHW);
-        else if (cw < WC - 1 && lane >= 64 - WL::LHW)
-            x.rdelta = G::RL * RW - (64 - 2 * WL::LHW);
-    }
-    if constexpr (GL::on) {
-        // the ring's DMA source: this lane's columns clamped into the row (a clamped lane
-        // holds columns outside the grid, whose cells emit nothing); LDS address = the low
-        // 32 bits of the LDS aperture address
-        const long long yc = y0 < 0 ? 0 : (y0 > A.pitch - C ? A.pitch - C : y0);
-#pragma unroll
-        for (int a = 0; a < NA; ++a) x.gsrc[a] = A.in[a] + (long long)(x.rA - K) * A.pitch + yc;
-        x.lds_pfr = &lds_g[0];
-        x.pf_lds = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)&lds_g[0]);
-        x.prow_max = x.rB - x.rA + 2 * K - 1;
-    }
-    x.partials = A.partials;
-    x.pbase = A.partial_base;
+    x.lds_in = p > 0 ? lds + (p - 1) * G::RL * RW : lds;
+    x.lds_out = p < P - 1 ? lds + p * G::RL * RW : lds;
     x.A = &A;
     if (MM_CHAIN_ASM) {  // register offsets of the chains' operands: 2 * attribute, 8 = pad
 #pragma unroll
@@ -1028,7 +751,6 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
             x.qib[t] = qu && A.post_b[t] >= 0 ? 2 * A.post_b[t] : 8;
         }
     }
-
     // every wave runs to iteration iend (a whole number of groups): the last wave emits
     // the segment's last row at iteration (P-1)*D + S0 + R - 1
     const int need = (P - 1) * G::D + G::S0 + (x.rB - x.rA);
@@ -1036,18 +758,109 @@ __global__ __launch_bounds__(64 * P * MM_WIDE_WC, MW) void mm_wide_kernel(const 
     // a strip whose loaded columns include the grid's first / last column or columns past
     // it fixes up the lanes holding them
     const bool edge = !(c0 >= 1 && c0 + 64 * C <= W - 1);
-    // partials unit of this wave: block * WC + column wave
     if (edge)
-        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, blk * WC + cw, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, iend, carry);
     else
-        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, blk * WC + cw, iend);
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, iend, carry);
+}
+
+// The linear plan (A.lin = 1): ONE round of workgroups, waves_total of them (the chip's
+// resident slots), each taking an equal share of the pass. The range's strips are laid
+// end to end in strip order, every row of an interior strip costing 2 units and of the two
+// edge strips (their slower edge body) A.lin_e2 units; workgroup b takes the rows whose
+// cost offset lies in [b*T/n, (b+1)*T/n) -- the tail of one strip and the head of the next,
+// or a run inside one -- as consecutive segments of at most A.lin_maxr rows (buffer
+// offsets below 2^31). Against one workgroup per fixed-length segment this drops the
+// partly filled last round of workgroups and most segment starts (each pays the pipeline
+// fill, (P-1)*D + S0 iterations): a thin slab's 936 segments of 683 rows on 512 slots took
+// two rounds of 735 iterations for 1204 rows of work per slot (mm_internal.hpp
+// lin_segments: the plan's arithmetic, shared with the engine).
+//
+// K = KW * P fused steps per launch of an NA-attribute one-pass program (NA = 1: one
+// diffusion; NA > 1: pre-chain, diffusions of the attributes in diffuse_mask, post-chain),
+// C columns per lane, MW waves per SIMD, P waves per workgroup. Work: the linear plan
+// (A.lin), or one workgroup per strip segment by mm_passk.hpp's seg_map with blocks in
+// place of waves -- the two edge strips first (A.th_edge rows), then the others (A.th
+// rows). RED: every level's sums of the workgroup's output cells into
+// partials[partial_base + block][K][NA]. NT & 1: non-temporal stores.
+template <int C, int NA, int KW, int P, int MW, int U, int B, bool RED, int NT>
+__global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
+    using G = WGeom<KW, P, B>;
+    constexpr int K = G::K;
+    constexpr int RW = 32 * C * NA;  // dv2 per LDS row
+    __shared__ dv2 lds[(P > 1 ? P - 1 : 1) * G::RL * RW];
+    const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // level group
+    const long long blk = blockIdx.x;
+    if (blk >= A.waves_total) return;  // the whole block: no barrier is left waiting
+    double carry[KW][NA];
+#pragma unroll
+    for (int q = 0; q < KW; ++q) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) carry[q][a] = 0.0;
+    }
+    // The workgroup's segments (strip, first row, end row) go through LDS: only the
+    // segment counter stays live across the segment loop (the plan's 64-bit arithmetic
+    // held through the hot loop cost it registers: 2x slower, round 5).
+    __shared__ int segs[kLinSegs][3];
+    __shared__ int nsegs;
+    if (threadIdx.x == 0) {
+        int ns = 0;
+        if (A.lin) {
+            ns = lin_segments(A, blk, segs, kLinSegs);
+            ns = ns < kLinSegs ? ns : kLinSegs;  // the engine plans at most kLinSegs
+        } else {
+            int rlo, rhi;
+            long long w = blk;
+            if (w < A.waves_a) {
+                rlo = A.ra0;
+                rhi = A.ra1;
+            } else {
+                w -= A.waves_a;
+                rlo = A.rb0;
+                rhi = A.rb1;
+            }
+            seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, segs[0][0], segs[0][1], segs[0][2]);
+            ns = 1;
+        }
+        nsegs = ns;
+    }
+    __syncthreads();
+    const int nseg = __builtin_amdgcn_readfirstlane(nsegs);
+    for (int si = 0; si < nseg; ++si) {
+        const int strip = __builtin_amdgcn_readfirstlane(segs[si][0]);
+        const int rA = __builtin_amdgcn_readfirstlane(segs[si][1]);
+        const int rB = __builtin_amdgcn_readfirstlane(segs[si][2]);
+        // The kernel arguments are re-read per segment (an opaque zero offset into the
+        // kernarg segment) and the lane index recomputed: hoisted out of this loop, their
+        // values were held through the steady loops, which then reloaded an LDS address
+        // from scratch every row (tools/asm_steady.py; a vmcnt(0) wait per row)
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        typedef const __attribute__((address_space(4))) PassArgs KArgs;
+        KArgs* ka = (KArgs*)((const __attribute__((address_space(4))) char*)
+                                 __builtin_amdgcn_kernarg_segment_ptr() + zero);
+        int ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        // (four attributes: A itself -- the chains' scalar operands must stay provably
+        // uniform for chain_asm's SGPR constraints)
+        const PassArgs& As = NA == 1 ? *(const PassArgs*)ka : A;
+        wide_segment<C, NA, KW, P, U, B, RED, NT>(As, lds, p, ln, strip, rA, rB, carry);
+    }
+    if (RED && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+        // partials[partial_base + block][K][NA]: this wave's KW levels (lane 0)
+#pragma unroll
+        for (int q = 0; q < KW; ++q) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a)
+                A.partials[((A.partial_base + blk) * K + p * KW + q) * NA + a] = carry[q][a];
+        }
+    }
 }
 
 template <int C, int NA, int KW, int P, int MW, int NT>
 hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     constexpr int U = MM_WIDE_U;
-    const long long blocks = wide_grid(a);
-    const dim3 g((unsigned)blocks), b(64 * P * MM_WIDE_WC);
+    const dim3 g((unsigned)a.waves_total), b(64 * P);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
         hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, true, NT>), g, b, 0, s, a);
@@ -1078,7 +891,7 @@ int wide_blocks_v() {
     }
     const int regs = (fa.numRegs + 7) / 8 * 8;
     const int waves_per_simd = regs > 0 ? std::min(8, 512 / regs) : 8;
-    int blocks = waves_per_simd * 4 / (P * MM_WIDE_WC);
+    int blocks = waves_per_simd * 4 / P;
     if (fa.sharedSizeBytes > 0) blocks = std::min(blocks, (int)(160 * 1024 / fa.sharedSizeBytes));
     return std::max(blocks, 0);
 }

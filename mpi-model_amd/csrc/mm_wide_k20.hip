@@ -24,8 +24,6 @@ int wide_blocks_k20(bool red, int nt) {
     return wide_blocks<4, 1, MM_K20_KW, 20 / MM_K20_KW, MM_WIDE_MIN_WAVES>(red, nt);
 }
 
-int wide_waves_k20() { return 20 / MM_K20_KW * MM_WIDE_WC; }
-
-int wide_wc_k20() { return MM_WIDE_WC; }
+int wide_waves_k20() { return 20 / MM_K20_KW; }
 
 }  // namespace mm

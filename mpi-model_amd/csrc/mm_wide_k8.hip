@@ -20,6 +20,5 @@ hipError_t wide_launch_k8(bool red, const PassArgs& a, hipStream_t s, int v) {
 
 int wide_blocks_k8(bool red, int nt) { return wide_blocks<4, 1, 2, 4, MM_WIDE_MIN_WAVES>(red, nt); }
 
-int wide_wc_k8() { return MM_WIDE_WC; }
 
 }  // namespace mm

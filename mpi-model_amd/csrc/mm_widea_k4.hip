@@ -2,7 +2,8 @@
 // and several attributes (config C5: four, with transfer chains): 2 columns per lane,
 // 1 level per wave, 4 waves per workgroup, rows handed on in groups of 2 (the LDS ring
 // of a group of 4 rows holds 96 KiB per workgroup). Pre- and post-chains with run-time
-// operands (chain_asm; a pass without one runs its four slots on the pad).
+// operands (chain_asm: the first n slots of a chain run, a scalar branch inside the asm
+// skips the rest; outflows leaving the system land on the pad pair).
 #ifndef MM_WIDE_U
 #define MM_WIDE_U 2
 #endif

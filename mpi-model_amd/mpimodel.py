@@ -22,6 +22,9 @@ MM_FILL_RANDOM = 1
 MM_HALO_NONE = 0
 MM_HALO_RCCL = 1
 MM_HALO_HOST = 2
+MM_CHAIN_NONE = 0  # mm_info.chain_kernel (include/mpimodel.h)
+MM_CHAIN_RING = 2
+MM_CHAIN_RUNTIME = 3
 SEED = 0x4D50494D
 
 # every symbol include/mpimodel.h declares

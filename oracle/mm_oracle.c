@@ -185,6 +185,123 @@ void or_field_step_slab(long long H, long long W, long long x_init, long long h,
     step_rows(H, W, x_init, x_init + h, grid_row, &c, vout, rate);
 }
 
+/* step_rows with the counts hoisted: rows strictly inside the grid have cnt == 8 except in
+ * their first and last column. Same operations, same order, same results. */
+#if defined(__x86_64__)
+#define OR_FAST_TARGET __attribute__((target("avx2,fma")))
+#else
+#define OR_FAST_TARGET
+#endif
+static OR_FAST_TARGET void s_row_fast(long long H, long long W, long long gx,
+                                      const double* vrow, double rate, double* s) {
+    if (vrow == NULL || gx < 0 || gx >= H || gx == 0 || gx == H - 1 || W < 3) {
+        s_row(H, W, gx, vrow, rate, s);
+        return;
+    }
+    const double r8 = rate * 0.125;
+    double d;
+    emit(rate, vrow[0], or_neighbor_count(H, W, gx, 0), &s[0], &d);
+    for (long long y = 1; y < W - 1; ++y) s[y] = vrow[y] * r8;
+    emit(rate, vrow[W - 1], or_neighbor_count(H, W, gx, W - 1), &s[W - 1], &d);
+}
+
+static OR_FAST_TARGET void step_rows_fast(long long H, long long W, long long x_lo,
+                                          long long x_hi, row_fn rows, const void* ctx,
+                                          double* vout, double rate) {
+    double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
+    if (!buf) return;
+    double* s_prev = buf;
+    double* s_cur = buf + W;
+    double* s_next = buf + 2 * W;
+    double* p = buf + 3 * W;
+    double* c3 = buf + 4 * W;
+    c3[0] = 0.0;
+    c3[W + 1] = 0.0;
+    s_row_fast(H, W, x_lo - 1, rows(ctx, x_lo - 1), rate, s_prev);
+    s_row_fast(H, W, x_lo, rows(ctx, x_lo), rate, s_cur);
+    for (long long x = x_lo; x < x_hi; ++x) {
+        s_row_fast(H, W, x + 1, rows(ctx, x + 1), rate, s_next);
+        for (long long y = 0; y < W; ++y) {
+            p[y] = s_prev[y] + s_next[y];
+            c3[y + 1] = p[y] + s_cur[y];
+        }
+        const double* v = rows(ctx, x);
+        double* o = vout + (x - x_lo) * W;
+        if (v == NULL) {
+            for (long long y = 0; y < W; ++y) o[y] = 0.0;
+        } else if (x > 0 && x < H - 1 && W >= 3) {
+            for (long long y = 0; y < W; y += W - 1) {  /* first and last column */
+                double sy, d;
+                emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
+                o[y] = d + ((c3[y] + c3[y + 2]) + p[y]);
+            }
+            for (long long y = 1; y < W - 1; ++y) {  /* cnt == 8: d = fma(s, -8, v) */
+                double d = fma(s_cur[y], -8.0, v[y]);
+                double nb = (c3[y] + c3[y + 2]) + p[y];
+                o[y] = d + nb;
+            }
+        } else {
+            for (long long y = 0; y < W; ++y) {
+                double sy, d;
+                emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
+                o[y] = d + ((c3[y] + c3[y + 2]) + p[y]);
+            }
+        }
+        double* t = s_prev;
+        s_prev = s_cur;
+        s_cur = s_next;
+        s_next = t;
+    }
+    free(buf);
+}
+
+static int fast_ok(void) {
+#if defined(__x86_64__)
+    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+#else
+    return 1;
+#endif
+}
+
+int or_field_rows(long long H, long long W, long long lo, long long hi, int steps,
+                  double rate, uint64_t seed, double* out) {
+    if (lo < 0) lo = 0;
+    if (hi > H) hi = H;
+    if (hi <= lo || W <= 0) return 0;
+    if (steps < 0) steps = 0;
+    const long long clo = lo - steps > 0 ? lo - steps : 0;
+    const long long chi = hi + steps < H ? hi + steps : H;
+    const size_t n = (size_t)((chi - clo) * W);
+    double* a = (double*)malloc(sizeof(double) * n);
+    double* b = (double*)malloc(sizeof(double) * n);
+    if (!a || !b) {
+        free(a);
+        free(b);
+        return -1;
+    }
+    or_fill_random(H, W, clo, chi - clo, seed, a);
+    const int fast = fast_ok();
+    long long plo = clo, phi = chi;  /* rows of `a` exact after the previous step */
+    for (int st = 1; st <= steps; ++st) {
+        const long long elo = lo - steps + st > 0 ? lo - steps + st : 0;
+        const long long ehi = hi + steps - st < H ? hi + steps - st : H;
+        grid_ctx c = {a, H, W, clo, plo, phi};
+        if (fast)
+            step_rows_fast(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate);
+        else
+            step_rows(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate);
+        double* t = a;
+        a = b;
+        b = t;
+        plo = elo;
+        phi = ehi;
+    }
+    memcpy(out, a + (lo - clo) * W, sizeof(double) * (size_t)((hi - lo) * W));
+    free(a);
+    free(b);
+    return 0;
+}
+
 void or_field_step_general(long long H, long long W, const double* v, const double* outf,
                            double* vout) {
     double* s = (double*)malloc(sizeof(double) * (size_t)(H * W));

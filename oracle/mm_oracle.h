@@ -96,6 +96,18 @@ typedef struct {
 void or_program_step(long long H, long long W, int n_attr, double* const* v,
                      const or_flow* flows, int n_flows, double* scratch);
 
+/* Rows [lo, hi) of the seeded random grid (or_fill_random) after `steps` whole-grid steps
+ * (or_field_step), computed on those rows' dependency cone only: the fill of rows
+ * [lo - steps, hi + steps), then step s on the rows still exact after it,
+ * [lo - steps + s, hi + steps - s) (clipped to the grid, whose edges are exact). The same
+ * operations as or_field_step in the same order -- bit-identical rows -- with the
+ * neighbour counts hoisted out of the interior rows and the explicit fma of the cnt == 8
+ * cells on the FMA instruction where the CPU has one. For full-size GPU checks
+ * (32768^2 x 20+ steps), run over row chunks in threads. Returns 0, or -1 if out of
+ * memory. */
+int or_field_rows(long long H, long long W, long long lo, long long hi, int steps,
+                  double rate, uint64_t seed, double* out);
+
 /* Neumaier-compensated sum (used for quick checks; tests use math.fsum). */
 double or_sum(const double* v, size_t n);
 

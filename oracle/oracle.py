@@ -75,6 +75,8 @@ def lib():
         L.or_field_step_slab.argtypes = [LL, LL, LL, LL, P, P, D]
         L.or_field_step_general.argtypes = [LL, LL, P, P, P]
         L.or_program_step.argtypes = [LL, LL, I, P, ctypes.POINTER(OrFlow), I, P]
+        L.or_field_rows.restype = I
+        L.or_field_rows.argtypes = [LL, LL, LL, LL, I, D, ctypes.c_uint64, P]
         L.or_sum.restype = D
         L.or_sum.argtypes = [P, ctypes.c_size_t]
         _lib = L
@@ -150,6 +152,34 @@ def field_step_slab(H, W, x_init, vg, rate):
     o = np.empty((h, W), dtype=np.float64)
     lib().or_field_step_slab(H, W, x_init, h, _ptr(vg), _ptr(o), rate)
     return o
+
+
+def field_rows(H, W, lo, hi, steps, rate, seed=SEED, threads=None, chunk=None):
+    """Rows [lo, hi) of fill_random(H, W) after `steps` field steps: or_field_rows on the
+    dependency cone of row chunks, the chunks in parallel threads (ctypes releases the GIL).
+    Bit-identical to field_step(fill_random(H, W), rate, steps)[lo:hi], at a cost that
+    fits full-size GPU checks (32768^2, 40 steps: ~1 min on 16 cores)."""
+    from concurrent.futures import ThreadPoolExecutor
+    lo, hi = max(0, lo), min(H, hi)
+    out = np.empty((max(hi - lo, 0), W), dtype=np.float64)
+    if hi <= lo:
+        return out
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    # chunks several times the cone's depth (the cone costs ~steps extra rows per chunk)
+    chunk = chunk or max(64, 8 * steps, -(-(hi - lo) // (4 * threads)))
+    starts = list(range(lo, hi, chunk))
+    L = lib()
+
+    def one(a):
+        b = min(hi, a + chunk)
+        view = out[a - lo:b - lo]
+        rc = L.or_field_rows(H, W, a, b, steps, rate, seed, view.ctypes.data_as(ctypes.c_void_p))
+        if rc != 0:
+            raise MemoryError(f"or_field_rows rows [{a}, {b}): out of memory")
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, starts))
+    return out
 
 
 def program_step(fields, flows, steps=1, sums_per_step=False):

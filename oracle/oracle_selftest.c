@@ -65,6 +65,24 @@ static void grid_case(long long H, long long W) {
             free(o);
         }
     }
+    /* the dependency-cone rows (or_field_rows) after 3 steps: every row range */
+    {
+        double* c = malloc(n * sizeof *c);
+        double* d = malloc(n * sizeof *d);
+        memcpy(c, v, n * sizeof *v);
+        for (int st = 0; st < 3; ++st) {
+            or_field_step(H, W, c, d, 0.3);
+            memcpy(c, d, n * sizeof *c);
+        }
+        for (long long lo = 0; lo < H; ++lo)
+            for (long long hi = lo + 1; hi <= H; hi += 2) {
+                CHECK(or_field_rows(H, W, lo, hi, 3, 0.3, 0x4D50494DULL, d) == 0, "rows alloc");
+                for (long long i = 0; i < (hi - lo) * W; ++i)
+                    CHECK(d[i] == c[lo * W + i], "rows %lldx%lld [%lld,%lld)", H, W, lo, hi);
+            }
+        free(c);
+        free(d);
+    }
     /* the reference's single-source application on every cell of small grids */
     if (H * W <= 64) {
         for (long long x = 0; x < H; ++x)

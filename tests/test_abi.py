@@ -22,6 +22,27 @@ def test_header_and_binding_agree(mm):
     assert declared_functions() == sorted(mm.EXPORTS)
 
 
+def test_header_constants_match_binding_and_engine(mm):
+    # every #define value of the boundary (flow kinds, fill modes, halo modes, the
+    # mm_info.chain_kernel codes) is the binding's, and the engine reports chain kernels
+    # by those names only (the GPU tests compare mm_engine_info with the binding's values)
+    text = open(os.path.join(REPO, "include", "mpimodel.h")).read()
+    defines = dict(re.findall(r"#define\s+(MM_[A-Z_]+)\s+(-?\d+)\b", text))
+    defines.update(re.findall(r"\b(MM_[A-Z_]+)\s*=\s*(-?\d+)", text))  # enumerators
+    for name in ("MM_CHAIN_NONE", "MM_CHAIN_RING", "MM_CHAIN_RUNTIME", "MM_FLOW_DIFFUSE",
+                 "MM_FLOW_TRANSFER", "MM_FILL_UNIFORM", "MM_FILL_RANDOM", "MM_HALO_NONE",
+                 "MM_HALO_RCCL", "MM_HALO_HOST", "MM_OK"):
+        assert name in defines, name
+        assert int(defines[name]) == getattr(mm, name), name
+    engine = open(os.path.join(REPO, "mpi-model_amd", "csrc", "mm_engine.hip")).read()
+    sets = re.findall(r"chain_kernel\s*=\s*([^;]+);", engine)
+    assert sets, "mm_engine_info no longer sets chain_kernel"
+    for v in sets:  # `cond ? A : B` or `A`: every value a name from the header
+        values = v.split("?", 1)[-1].split(":")
+        assert all(x.strip() in ("MM_CHAIN_NONE", "MM_CHAIN_RING", "MM_CHAIN_RUNTIME")
+                   for x in values), v
+
+
 def test_library_exports_every_declared_symbol(mm):
     L = mm.lib()
     for name in declared_functions():

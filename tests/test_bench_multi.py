@@ -88,7 +88,7 @@ def test_valu_roof_four_attributes():
     import bench
     assert bench.level_row_cycles(4) == 120
     assert bench.level_row_cycles(2, 4, 4, 2) == 4 * (56 + 8) + 4 * 2 * 12 == 352
-    assert bench.level_row_cycles(2, 4, 4, 1) == 352 + 4 * 2 * 16
+    assert bench.level_row_cycles(2, 4, 4, 3) == 352
     h, W = 4096, 4096
     info = dict(INFO, chain_kernel=2, steps_per_launch=8)
     lr = lambda k, cols: bench.level_row_cycles(cols, 4, 4, 2 if k == 8 else 1)  # noqa: E731

@@ -195,9 +195,11 @@ def test_mid_slab_in_a_chain_takes_the_k20_planner(gpu):
         assert e.pass_plan(20) == [7, 7, 6] and e.info()["kernel"] == 2
 
 
-def test_c3_eight_gpu_slab_shape(gpu, O, monkeypatch):
-    """The 4096 x 32768 slab one GPU of an 8-GPU c3 run holds (2^27 cells): the default
-    planner's 20 steps are mm_passk_kernel passes of 7 + 7 + 6."""
+def test_standalone_mid_slab_keeps_passk(gpu, O, monkeypatch):
+    """A standalone 4096 x 32768 grid (2^27 cells, NO halo -- not the slab of an N = 8 c3
+    rank: that one takes the level-split kernel's K = 20 pass with the interior / border
+    split, tests/test_gpu_fullsize.py c3_n8): the default planner's 20 steps are
+    mm_passk_kernel passes of 7 + 7 + 6."""
     driver_run_bands(gpu, O, monkeypatch, 4096, 32768, 0, [7, 7, 6])
 
 
@@ -208,8 +210,9 @@ C5_FLOWS = [(2, 0, 1, 0.05), (2, 1, 2, 0.03), (2, 2, 3, 0.02), (2, 3, 0, 0.01),
 C5_REORDERED = [C5_FLOWS[1], C5_FLOWS[0], C5_FLOWS[2], C5_FLOWS[3]] + C5_FLOWS[4:]
 
 
-@pytest.mark.parametrize("flows,chain,env", [(C5_FLOWS, 2, {}), (C5_REORDERED, 3, {}),
-                                             (C5_FLOWS, 3, {"MM_CHAIN_RING": "0"})],
+@pytest.mark.parametrize("flows,chain,env", [(C5_FLOWS, "MM_CHAIN_RING", {}),
+                                             (C5_REORDERED, "MM_CHAIN_RUNTIME", {}),
+                                             (C5_FLOWS, "MM_CHAIN_RUNTIME", {"MM_CHAIN_RING": "0"})],
                          ids=["ring", "reordered", "ring_runtime_operands"])
 def test_c5_bench_size_bit_exact(gpu, O, monkeypatch, flows, chain, env):
     """bench.py's C5 configuration at its own size (4096^2, 4 attributes, per-step sums,
@@ -233,7 +236,7 @@ def test_c5_bench_size_bit_exact(gpu, O, monkeypatch, flows, chain, env):
         add_flows(e, flows)
         info = e.info()
         assert info["kernel"] == 3 and info["steps_per_launch"] == 8, info
-        assert info["chain_kernel"] == chain, info
+        assert info["chain_kernel"] == getattr(gpu, chain), info
         assert e.pass_plan(21) == [8, 8, 4, 1]
         e.run(21, reduce_every=1)
         want, sums = O.program_step(fields, flows, steps=21, sums_per_step=True)

@@ -200,9 +200,14 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1},
-    # XCD-chunked block order (off by default): the same cells, blocks on other XCDs
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_CHUNK": 16},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_XCD_CHUNK": 2}]
+    # the linear plan (one round of workgroups sharing the pass; auto on large slabs),
+    # forced on these small grids: workgroups spanning strips, segments cut at MM_LIN_MAXR
+    # rows, more workgroups than rows (some run nothing), edge rows at the interior cost
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_LIN": 1},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_LIN": 1, "MM_LIN_WORKERS": 7},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_LIN": 1, "MM_LIN_WORKERS": 3, "MM_LIN_MAXR": 17},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_LIN": 1, "MM_LIN_WORKERS": 600, "MM_SEG_EDGE": 1.0},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4, "MM_LIN": 1, "MM_LIN_WORKERS": 2, "MM_KERNEL_VARIANT": 1}]
 
 
 def env_id(env):
@@ -243,7 +248,9 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
 @pytest.mark.parametrize("env", [{}, {"MM_WIDE": 0}]
                          + [{"MM_WIDE": 0, "MM_STEPS_PER_PASS": k} for k in (3, 2, 8, 6, 7, 10)]
                          + [{"MM_PASSK": 0}]
-                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)]
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k, "MM_LIN": 1, "MM_LIN_WORKERS": w,
+                             "MM_LIN_MAXR": 40} for k, w in ((20, 5), (8, 64))],
                          ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
@@ -417,7 +424,7 @@ def test_flow_program_wide_kernel(gpu, O, monkeypatch, env, prog, shape):
     k = int(env.get("MM_STEPS_PER_PASS", 8))
     # K = 8: the ring instance for C5's chain, the run-time-operand chain otherwise
     ring = prog == 0 and k == 8 and env.get("MM_CHAIN_RING", 1) != 0
-    assert e.info()["chain_kernel"] == (2 if ring else 3)
+    assert e.info()["chain_kernel"] == (gpu.MM_CHAIN_RING if ring else gpu.MM_CHAIN_RUNTIME)
     plan = e.pass_plan(steps)
     assert sum(plan) == steps and plan[0] == k
     assert all(e.pass_kernel(p)[0] == (3 if p in (4, 8) else 2) for p in plan)

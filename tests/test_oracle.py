@@ -115,6 +115,19 @@ def test_slab_decomposition_is_bit_exact(O, H, G):
     assert np.array_equal(np.vstack(parts), want)
 
 
+@pytest.mark.parametrize("H,W,steps", [(1, 1, 3), (2, 5, 2), (3, 3, 4), (5, 1, 3), (1, 7, 2),
+                                       (37, 130, 7), (64, 300, 20), (130, 257, 9), (300, 700, 25)])
+def test_field_rows_cone_is_the_full_step(O, H, W, steps):
+    # or_field_rows (the full-size GPU tests' checker: rows on their dependency cone, the
+    # counts hoisted, the fma on the FMA unit, row chunks in threads) against or_field_step
+    # on the whole grid, bit for bit, for row ranges at both edges, inside, and one row
+    want = O.field_step(O.fill_random(H, W), 0.3, steps=steps)
+    for lo, hi in ((0, H), (H // 3, H - H // 4), (H - 1, H), (0, 1), (H // 2, H // 2 + 1)):
+        for chunk in (None, 1, 5):
+            got = O.field_rows(H, W, lo, hi, steps, 0.3, chunk=chunk)
+            assert np.array_equal(got, want[lo:hi]), (H, W, steps, lo, hi, chunk)
+
+
 @pytest.mark.parametrize("H,W,P,steps", [(37, 29, 3, 5), (16, 130, 4, 3), (9, 7, 2, 4)])
 def test_cpu_mpi_baseline_is_the_oracle(O, tmp_path, H, W, P, steps):
     """The MPI CPU baseline (oracle/mm_cpu_mpi.c, bench.py's cpu_baseline leg) reproduces the

@@ -9,6 +9,8 @@
 #                                             rocprofv3 --kernel-trace --stats of bench.py,
 #                                             then two PMC passes (FETCH_SIZE, WRITE_SIZE),
 #                                             summarised by tools/prof_summary.py
+#   bash tools/gpu.sh trace NAME WL STEPS WARMUP [bench.py args]
+#                                             rocprofv3 --kernel-trace only (per-dispatch timeline)
 #   bash tools/gpu.sh sq NAME WL STEPS WARMUP [bench.py args]
 #                                             SQ wave-cycle split + effective clock (PMC)
 #   bash tools/gpu.sh pmc NAME WL STEPS WARMUP "COUNTERS" [bench.py args]
@@ -16,6 +18,14 @@
 #   bash tools/gpu.sh selfhalo                bench.py --self-halo beside the plain run on the
 #                                             slab shapes of the N > 1 runs (price of the
 #                                             interior / border split + RCCL exchange)
+#   bash tools/gpu.sh final                   a round's evidence on the committed tree: test, lines,
+#                                             then prof of each line's own plan and length
+#   bash tools/gpu.sh ab TAG WL STEPS REPS "ENV_A" "ENV_B" [bench.py args]
+#                                             A/B of two environments on one box, alternating
+#                                             A B A B ... REPS times (GCUPS per run)
+#   bash tools/gpu.sh thin                    segment-plan sweep of the thin split slabs of the
+#                                             c3 N = 8 / N = 4 runs (4096 / 8192 x 32768,
+#                                             self-halo, 200 steps) against the 32768^2 slab
 #   bash tools/gpu.sh scale WL [N...]         the driver's multi-GPU command, N = 1 2 4 8 by
 #                                             default (needs N GPUs; never run on the 1-GPU box)
 #
@@ -69,6 +79,17 @@ prof() {  # NAME WL STEPS WARMUP [args]
     python3 tools/prof_summary.py "$out" "$wl" > "$out/summary.json" && cat "$out/summary.json"
 }
 
+trace() {  # NAME WL STEPS WARMUP [args]
+    local name=$1 wl=$2 steps=$3 warm=$4
+    shift 4
+    local out="$D/trace_$name"
+    mkdir -p "$out"
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run \
+        -- python3 bench.py --workload "$wl" --steps "$steps" --warmup "$warm" --no-cpu-baseline "$@" \
+        > "$out/trace.log" 2>&1 || fail "trace $name" $? "$out/trace.log"
+    grep '^{' "$out/trace.log" | cut -c1-200
+}
+
 sq() {  # NAME WL STEPS WARMUP [args]: SQ wave-cycle split + effective clock (one --pmc pass:
         # 6 SQ + 1 GRBM counters fit gfx950's slots), after a trace run for the kernel time
     local name=$1 wl=$2 steps=$3 warm=$4
@@ -109,6 +130,43 @@ selfhalo() {
     done
 }
 
+final() {
+    gpu_test
+    lines
+    prof c3_k20 c3 20 5
+    prof c4_k20 c4 1000 50
+    prof c2_k8 c2 1000 50
+    prof c5_k8 c5 1000 50
+}
+
+ab() {  # TAG WL STEPS REPS ENVA ENVB [args]
+    local tag=$1 wl=$2 steps=$3 reps=$4 ea=$5 eb=$6 r
+    shift 6
+    for ((r = 0; r < reps; r++)); do
+        env $ea TAG="${tag}_A$r" bash "$0" bench "$wl" "$steps" 5 --no-cpu-baseline "$@" | \
+            python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('A', '$ea', d['value'], d['roofline']['kernel_avg_us'])"
+        env $eb TAG="${tag}_B$r" bash "$0" bench "$wl" "$steps" 5 --no-cpu-baseline "$@" | \
+            python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('B', '$eb', d['value'], d['roofline']['kernel_avg_us'])"
+    done
+}
+
+thin() {
+    local steps=${THIN_STEPS:-200} v
+    TAG=32768x32768_plain bench c3 $steps 5 --no-cpu-baseline
+    for g in "4096 32768" "8192 32768"; do
+        set -- $g
+        TAG="${1}x${2}_self" bench c3 $steps 5 --grid $1 $2 --no-cpu-baseline --self-halo
+        for v in ${THIN_SW:-1 2 3 6}; do
+            MM_SEG_WAVES=$v TAG="${1}x${2}_self_sw$v" bench c3 $steps 5 --grid $1 $2 \
+                --no-cpu-baseline --self-halo
+        done
+        for v in ${THIN_K:-12 16}; do
+            MM_STEPS_PER_PASS=$v TAG="${1}x${2}_self_k$v" bench c3 $steps 5 --grid $1 $2 \
+                --no-cpu-baseline --self-halo
+        done
+    done
+}
+
 scale() {  # WL [N...]
     local wl=$1
     shift
@@ -130,8 +188,12 @@ case "$cmd" in
     lines) lines ;;
     prof) prof "$@" ;;
     sq) sq "$@" ;;
+    trace) trace "$@" ;;
     pmc) pmc "$@" ;;
     selfhalo) selfhalo ;;
+    thin) thin ;;
+    ab) ab "$@" ;;
+    final) final ;;
     scale) scale "$@" ;;
     *) echo "unknown command $cmd"; exit 2 ;;
 esac
