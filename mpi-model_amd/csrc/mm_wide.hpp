@@ -110,6 +110,9 @@ struct WLane {
     int sy[C];      // column spans of this lane's columns
     int cnt[C];     // neighbour counts of the columns in an interior row (8 / 5 / 0 ...)
     bool special;   // some column of this lane has cnt != 8 (edge strips only)
+    bool eL, eR;    // EDGE body: this lane holds the grid's first column as its column 0 /
+                    // its last column as its column C-1
+    bool gen;       // (wave-uniform) a strip the EDGE body cannot run: every group GEN
     bool own[C];    // output cells of this workgroup
     double ownw[C]; // own as 1.0 / 0.0 (RED: the weights of the all-rows-owned groups)
 };
@@ -122,9 +125,14 @@ struct WinC {
 };
 
 // s and d of this lane's columns of row gx (oracle/mm_oracle.c emit). FAST: interior
-// row of an interior strip (cnt == 8: s = u*(r/8), d = fma(s, -8, u)). EDGE: interior row;
-// the lanes holding an edge / outside column redo those columns with their true count.
-// GEN: any row (the row class is wave-uniform).
+// row of an interior strip (cnt == 8: s = u*(r/8), d = fma(s, -8, u)). EDGE: interior row
+// of a strip holding the grid's first (or last) column as a lane's column 0 (C-1), the
+// columns past it in whole lanes: every lane divides that column's out by its 5
+// neighbours, the lane holding it keeps the result -- no branch (the branches of the
+// per-lane fix-up below cost the edge strips 3.7x the rows' time, round 5); the columns
+// past the grid compute anything, and wemit keeps it from crossing into the grid. GEN:
+// any row and strip (the row class is wave-uniform; lanes redo their columns whose count
+// is not 8).
 template <int C, int BODY>
 __device__ __forceinline__ void procc(const WLane<C>& c, double r, double r8, long long gx,
                                       const double (&u)[C], double (&s)[C], double (&d)[C]) {
@@ -135,7 +143,16 @@ __device__ __forceinline__ void procc(const WLane<C>& c, double r, double r8, lo
             s[k] = u[k] * r8;
             d[k] = __builtin_fma(s[k], -8.0, u[k]);
         }
-        if (BODY != kBodyFast && c.special) {
+        if (BODY == kBodyEdge) {
+            const double us = c.eL ? u[0] : u[C - 1];
+            const double out = r * us;
+            const double sd = out / 5.0;  // oracle emit: cnt 5, s = out / cnt, d = u - out
+            const double dd = us - out;
+            s[0] = c.eL ? sd : s[0];
+            d[0] = c.eL ? dd : d[0];
+            s[C - 1] = c.eR ? sd : s[C - 1];
+            d[C - 1] = c.eR ? dd : d[C - 1];
+        } else if (BODY == kBodyGen && c.special) {
 #pragma unroll
             for (int k = 0; k < C; ++k)
                 if (c.cnt[k] != 8) emit_k(r, u[k], c.cnt[k], s[k], d[k]);
@@ -181,8 +198,12 @@ __device__ __forceinline__ void wemit(const WLane<C>& c, double r, double r8, lo
         p[k] = w.sp[k] + sn[k];
         c3[k] = p[k] + w.sc[k];
     }
-    const double left = dpp_lower(c3[C - 1]);  // c3 of column y0-1 (lane-1's last column)
-    const double right = dpp_upper(c3[0]);     // c3 of column y0+C (lane+1's first column)
+    double left = dpp_lower(c3[C - 1]);  // c3 of column y0-1 (lane-1's last column)
+    double right = dpp_upper(c3[0]);     // c3 of column y0+C (lane+1's first column)
+    if (BODY == kBodyEdge) {  // outside the grid s = 0, so c3 = 0 there (EDGE: see procc)
+        left = c.eL ? 0.0 : left;
+        right = c.eR ? 0.0 : right;
+    }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         const double cl = k == 0 ? left : c3[k - 1];
@@ -647,6 +668,7 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
     long long f1 = hi <= s ? s : s + (hi - s) / B * B;
     f0 = min(f0, (long long)iend);
     f1 = max(f0, min(f1, (long long)iend));
+    if (MID == kBodyEdge && x.c.gen) f0 = f1 = iend;  // a strip the EDGE body cannot run
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
     if (RED) {
         // inside the interior groups, those whose every level's output row lies in
@@ -756,12 +778,17 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
     const int need = (P - 1) * G::D + G::S0 + (x.rB - x.rA);
     const int iend = (need + G::B - 1) / G::B * G::B;
     // a strip whose loaded columns include the grid's first / last column or columns past
-    // it fixes up the lanes holding them
-    const bool edge = !(c0 >= 1 && c0 + 64 * C <= W - 1);
-    if (edge)
-        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, iend, carry);
-    else
+    // it: EDGE when it holds one of the two as a lane's column 0 / C-1 (the first column
+    // always is: c0 % C == 0; the last one when W % C == 0), GEN otherwise
+    const bool hasL = c0 < 1, hasR = c0 + 64 * C - 1 >= W - 1;
+    x.c.eL = hasL && y0 == 0;
+    x.c.eR = hasR && y0 + C - 1 == W - 1;
+    // (both, or the last column inside a lane: GEN for every group, the old fix-up)
+    x.c.gen = (hasL && hasR) || (hasR && (W - 1 - c0) % C != C - 1);
+    if (!hasL && !hasR)
         wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyFast>(x, iend, carry);
+    else
+        wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, iend, carry);
 }
 
 // The linear plan (A.lin = 1): ONE round of workgroups, waves_total of them (the chip's
