@@ -200,7 +200,10 @@ __device__ __forceinline__ void wemit(const WLane<C>& c, double r, double r8, lo
     }
     double left = dpp_lower(c3[C - 1]);  // c3 of column y0-1 (lane-1's last column)
     double right = dpp_upper(c3[0]);     // c3 of column y0+C (lane+1's first column)
-    if (BODY == kBodyEdge) {  // outside the grid s = 0, so c3 = 0 there (EDGE: see procc)
+    if (BODY != kBodyFast) {
+        // outside the grid s = 0, so c3 = 0 there: EDGE rows compute anything in the lanes
+        // past the grid (procc), and GEN rows of the same strip still hold such shares in
+        // their windows from the EDGE rows before them
         left = c.eL ? 0.0 : left;
         right = c.eR ? 0.0 : right;
     }
