@@ -53,20 +53,13 @@ __device__ __forceinline__ double share_of(double out, int cnt) {
     return cnt == 8 ? out * 0.125 : (cnt > 0 ? out / (double)cnt : 0.0);
 }
 
-// One emitter of the whole-grid step (oracle/mm_oracle.c emit): share s and kept value
-// d = u - out; cnt == 8 as s = u*(r/8), d = fma(s, -8, u).
-__device__ __forceinline__ void emit_one(double r, double u, int cnt, double& s, double& d) {
-    if (cnt == 8) {
-        s = u * (r * 0.125);
-        d = __builtin_fma(s, -8.0, u);
-    } else if (cnt > 0) {
-        const double out = r * u;
-        s = out / (double)cnt;
-        d = u - out;
-    } else {
-        s = 0.0;
-        d = u;
-    }
+// A neighbour's weight in the whole-grid step (oracle/mm_oracle.c c8_of): w = u * 8/cnt,
+// u itself for cnt == 8, 0 outside the grid -- each neighbour's share out/cnt is (r/8) * w.
+__device__ __forceinline__ double c8_one(int cnt) {
+    return cnt == 8 ? 1.0
+                    : (cnt == 5 ? 8.0 / 5.0
+                                : (cnt == 3 ? 8.0 / 3.0
+                                            : (cnt == 2 ? 4.0 : (cnt == 1 ? 8.0 : 0.0))));
 }
 
 // Chain entries are read with compile-time indices only, so they are scalar loads of
@@ -102,11 +95,13 @@ struct RawRow {
     double v0[NA], v1[NA], ve[NA];
 };
 
-// Processed row: shares (three columns) and u - out (two columns).
+// Processed row: weights (three columns), values and the self coefficient (-8, or 0 for a
+// cell without neighbours) of the two own columns.
 template <int NA>
 struct ProcRow {
-    double s0[NA], s1[NA], se[NA];
-    double d0[NA], d1[NA];
+    double w0[NA], w1[NA], we[NA];
+    double u0[NA], u1[NA];
+    double m0, m1;
 };
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -160,49 +155,31 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
         apply_chain<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
         apply_chain<NA>(ue, A.npre, A.pre_a, A.pre_b, A.pre_r);
     }
-    if (sx == 0) {  // row outside the global grid: emits nothing
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            o.s0[a] = o.s1[a] = o.se[a] = 0.0;
-            o.d0[a] = u0[a];
-            o.d1[a] = u1[a];
-        }
-        return;
-    }
-    if (sx == 3 && fast_cols) {  // interior rows and columns: cnt == 8 everywhere
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            if (A.diffuse_mask & (1 << a)) {
-                const double r8 = A.drate[a] * 0.125;
-                o.s0[a] = u0[a] * r8;
-                o.s1[a] = u1[a] * r8;
-                o.se[a] = ue[a] * r8;
-                o.d0[a] = __builtin_fma(o.s0[a], -8.0, u0[a]);
-                o.d1[a] = __builtin_fma(o.s1[a], -8.0, u1[a]);
-            } else {
-                o.s0[a] = o.s1[a] = o.se[a] = 0.0;
-                o.d0[a] = u0[a];
-                o.d1[a] = u1[a];
-            }
-        }
-        return;
-    }
-    const int c0 = (sx && sy0) ? sx * sy0 - 1 : 0;
-    const int c1 = (sx && sy1) ? sx * sy1 - 1 : 0;
-    const int ce = (sx && sye) ? sx * sye - 1 : 0;
+    o.m0 = (sx && sx * sy0 == 1) ? 0.0 : -8.0;
+    o.m1 = (sx && sx * sy1 == 1) ? 0.0 : -8.0;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        if (A.diffuse_mask & (1 << a)) {
-            const double r_ = A.drate[a];
-            double de;
-            emit_one(r_, u0[a], c0, o.s0[a], o.d0[a]);
-            emit_one(r_, u1[a], c1, o.s1[a], o.d1[a]);
-            emit_one(r_, ue[a], ce, o.se[a], de);
-        } else {
-            o.s0[a] = o.s1[a] = o.se[a] = 0.0;
-            o.d0[a] = u0[a];
-            o.d1[a] = u1[a];
+        o.u0[a] = u0[a];
+        o.u1[a] = u1[a];
+    }
+    if (sx == 3 && fast_cols) {  // interior rows and columns: cnt == 8 everywhere, w = u
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const bool dif = A.diffuse_mask & (1 << a);
+            o.w0[a] = dif ? u0[a] : 0.0;
+            o.w1[a] = dif ? u1[a] : 0.0;
+            o.we[a] = dif ? ue[a] : 0.0;
         }
+        return;
+    }
+    // (sx == 0: a row outside the global grid weighs 0)
+    const double c0 = c8_one(sx * sy0 - 1), c1 = c8_one(sx * sy1 - 1), ce = c8_one(sx * sye - 1);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        const bool dif = A.diffuse_mask & (1 << a);
+        o.w0[a] = dif ? u0[a] * c0 : 0.0;
+        o.w1[a] = dif ? u1[a] * c1 : 0.0;
+        o.we[a] = dif ? ue[a] * ce : 0.0;
     }
 }
 
@@ -215,19 +192,20 @@ __device__ __forceinline__ void emit_row(const PassArgs& A, int r, int rmax, uns
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (A.diffuse_mask & (1 << a)) {
-            const double p0 = P.s0[a] + N.s0[a];
-            const double p1 = P.s1[a] + N.s1[a];
-            const double pe = P.se[a] + N.se[a];
-            const double c0 = p0 + C.s0[a];
-            const double c1 = p1 + C.s1[a];
-            const double ce = pe + C.se[a];
-            const double left = dpp_from_lower_lane(c1, ce);   // c3 at column y0-1
-            const double right = dpp_from_upper_lane(c0, ce);  // c3 at column y0+2
-            w0[a] = C.d0[a] + ((left + c1) + p0);
-            w1[a] = C.d1[a] + ((c0 + right) + p1);
+            const double p0 = P.w0[a] + N.w0[a];
+            const double p1 = P.w1[a] + N.w1[a];
+            const double pe = P.we[a] + N.we[a];
+            const double c0 = p0 + C.w0[a];
+            const double c1 = p1 + C.w1[a];
+            const double ce = pe + C.we[a];
+            const double left = dpp_from_lower_lane(c1, ce);   // cw at column y0-1
+            const double right = dpp_from_upper_lane(c0, ce);  // cw at column y0+2
+            const double r8 = A.drate[a] * 0.125;
+            w0[a] = __builtin_fma(__builtin_fma(C.u0[a], C.m0, (left + c1) + p0), r8, C.u0[a]);
+            w1[a] = __builtin_fma(__builtin_fma(C.u1[a], C.m1, (c0 + right) + p1), r8, C.u1[a]);
         } else {
-            w0[a] = C.d0[a];
-            w1[a] = C.d1[a];
+            w0[a] = C.u0[a];
+            w1[a] = C.u1[a];
         }
     }
     if (CHAIN && A.npost) {
@@ -255,12 +233,14 @@ template <int NA>
 __device__ __forceinline__ void copy_row(ProcRow<NA>& d, const ProcRow<NA>& s) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        d.s0[a] = s.s0[a];
-        d.s1[a] = s.s1[a];
-        d.se[a] = s.se[a];
-        d.d0[a] = s.d0[a];
-        d.d1[a] = s.d1[a];
+        d.w0[a] = s.w0[a];
+        d.w1[a] = s.w1[a];
+        d.we[a] = s.we[a];
+        d.u0[a] = s.u0[a];
+        d.u1[a] = s.u1[a];
     }
+    d.m0 = s.m0;
+    d.m1 = s.m1;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {

@@ -152,20 +152,13 @@ __device__ __forceinline__ int span3k(long long n, long long i) {
     return (i >= 0 && i < n) ? 1 + (i > 0) + (i < n - 1) : 0;
 }
 
-// One emitter (oracle/mm_oracle.c emit): share s and kept value d = u - out; cnt == 8 as
-// s = u*(r/8), d = fma(s, -8, u) (equal to out/8 and u - out whenever out = r*u is normal).
-__device__ __forceinline__ void emit_k(double r, double u, int cnt, double& s, double& d) {
-    if (cnt == 8) {
-        s = u * (r * 0.125);
-        d = __builtin_fma(s, -8.0, u);
-    } else if (cnt > 0) {
-        const double out = r * u;
-        s = out / (double)cnt;
-        d = u - out;
-    } else {
-        s = 0.0;
-        d = u;
-    }
+// A neighbour's weight factor 8/cnt (oracle/mm_oracle.c c8_of: w = u * 8/cnt, 1 for an
+// interior cell, 0 outside the grid): the correctly rounded quotients as constants.
+__device__ __forceinline__ double c8k(int cnt) {
+    return cnt == 8 ? 1.0
+                    : (cnt == 5 ? 8.0 / 5.0
+                                : (cnt == 3 ? 8.0 / 3.0
+                                            : (cnt == 2 ? 4.0 : (cnt == 1 ? 8.0 : 0.0))));
 }
 
 // Descriptor of `rows` consecutive rows starting at `first` (pointer already offset):
@@ -197,10 +190,10 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, unsigned off
                                            (NT & 1) ? 2 : 0);
 }
 
-// One level's three-row window of one attribute: shares of the row above (p), shares
-// and u - out of the current row (c).
+// One level's three-row window of one attribute: the weights of the row above (wa) and of
+// the current row (wm), the current row's values (um).
 struct Win {
-    double sp0, sp1, sc0, sc1, dc0, dc1;
+    double wa0, wa1, wm0, wm1, um0, um1;
 };
 
 // What every level of one wave needs besides its windows.
@@ -242,13 +235,14 @@ __device__ __forceinline__ void chain_k(double (&u)[NA], int n, const signed cha
     for (int k = 0; k < NA; ++k) u[k] = v[k];
 }
 
-// Pre-chain, then per diffusing attribute out = rate*u, s = out/cnt, d = u - out for this
-// lane's two columns of row gx (src/Exponencial.hpp:18-20, src/Model.hpp:199); cells
-// outside the grid emit nothing; attributes that do not diffuse pass through (s = 0).
+// Pre-chain, then per diffusing attribute the weights w = u * 8/cnt of this lane's two
+// columns of row gx (oracle/mm_oracle.c w_row: each neighbour's share out/cnt = (r/8) * w,
+// src/Exponencial.hpp:18-20, src/Model.hpp:199); cells outside the grid weigh 0;
+// attributes that do not diffuse pass through (w = 0).
 template <int NA, bool FAST, bool CHAIN>
 __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long long gx,
-                                       double (&u0)[NA], double (&u1)[NA], double (&s0)[NA],
-                                       double (&s1)[NA], double (&d0)[NA], double (&d1)[NA]) {
+                                       double (&u0)[NA], double (&u1)[NA], double (&w0)[NA],
+                                       double (&w1)[NA]) {
     if (CHAIN && A.npre) {
         chain_k<NA>(u0, A.npre, A.pre_a, A.pre_b, A.pre_r);
         chain_k<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
@@ -258,27 +252,13 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (NA > 1 && !((A.diffuse_mask >> a) & 1)) {
-            s0[a] = s1[a] = 0.0;
-            d0[a] = u0[a];
-            d1[a] = u1[a];
-            continue;
-        }
-        const double r = A.drate[a];
-        if (inner) {  // interior row, interior strip: cnt == 8 (oracle/mm_oracle.c emit)
-            const double r8 = r * 0.125;
-            s0[a] = u0[a] * r8;
-            s1[a] = u1[a] * r8;
-            d0[a] = __builtin_fma(s0[a], -8.0, u0[a]);
-            d1[a] = __builtin_fma(s1[a], -8.0, u1[a]);
-        } else if (sx == 0) {  // row outside the grid
-            s0[a] = s1[a] = 0.0;
-            d0[a] = u0[a];
-            d1[a] = u1[a];
+            w0[a] = w1[a] = 0.0;
+        } else if (inner) {  // interior row, interior strip: cnt == 8, w = u
+            w0[a] = u0[a];
+            w1[a] = u1[a];
         } else {
-            const int k0 = c.sy0 ? sx * c.sy0 - 1 : 0;
-            const int k1 = c.sy1 ? sx * c.sy1 - 1 : 0;
-            emit_k(r, u0[a], k0, s0[a], d0[a]);
-            emit_k(r, u1[a], k1, s1[a], d1[a]);
+            w0[a] = u0[a] * c8k(sx * c.sy0 - 1);
+            w1[a] = u1[a] * c8k(sx * c.sy1 - 1);
         }
     }
 }
@@ -287,60 +267,65 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
 template <int NA, bool FAST, bool CHAIN>
 __device__ __forceinline__ void level_fill(const PassArgs& A, const Lane& c, long long gx, int m,
                                            Win (&w)[NA], double (&u0)[NA], double (&u1)[NA]) {
-    double s0[NA], s1[NA], d0[NA], d1[NA];
-    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, s0, s1, d0, d1);
+    double w0[NA], w1[NA];
+    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, w0, w1);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (m == 0) {
-            w[a].sp0 = s0[a];
-            w[a].sp1 = s1[a];
+            w[a].wa0 = w0[a];
+            w[a].wa1 = w1[a];
         } else {
-            w[a].sc0 = s0[a];
-            w[a].sc1 = s1[a];
-            w[a].dc0 = d0[a];
-            w[a].dc1 = d1[a];
+            w[a].wm0 = w0[a];
+            w[a].wm1 = w1[a];
+            w[a].um0 = u0[a];
+            w[a].um1 = u1[a];
         }
     }
 }
 
 // Level input row m >= 2 (global row gx): emit the windows' current row (then the
 // post-chain) and slide the windows.
-// v' = (u - out) + nb, nb = (c3(y-1) + c3(y+1)) + p with p = s(x-1) + s(x+1) and
-// c3 = p + s(x) (src/Model.hpp:206-211,234; the order fixed by oracle/mm_oracle.h).
+// v' = fma(fma(u, -8, W8), r/8, u), W8 = (cw(y-1) + cw(y+1)) + pw with pw = w(x-1) + w(x+1)
+// and cw = pw + w(x) (src/Model.hpp:206-211,234; the order fixed by oracle/mm_oracle.h); a
+// cell without neighbours (a 1 x 1 grid) keeps its value.
 template <int NA, bool FAST, bool CHAIN>
 __device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, long long gx,
                                            Win (&w)[NA], double (&u0)[NA], double (&u1)[NA],
-                                           double (&w0)[NA], double (&w1)[NA]) {
-    double sn0[NA], sn1[NA], dn0[NA], dn1[NA];
-    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, sn0, sn1, dn0, dn1);
+                                           double (&o0)[NA], double (&o1)[NA]) {
+    double wn0[NA], wn1[NA];
+    proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, wn0, wn1);
+    const int sxm = FAST ? 3 : span3k(c.H, gx - 1);  // the emitted row
+    const double m0 = (!FAST && sxm * c.sy0 == 1) ? 0.0 : -8.0;
+    const double m1 = (!FAST && sxm * c.sy1 == 1) ? 0.0 : -8.0;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (NA > 1 && !((A.diffuse_mask >> a) & 1)) {
-            w0[a] = w[a].dc0;
-            w1[a] = w[a].dc1;
+            o0[a] = w[a].um0;
+            o1[a] = w[a].um1;
         } else {
-            const double p0 = w[a].sp0 + sn0[a], p1 = w[a].sp1 + sn1[a];
-            const double c0 = p0 + w[a].sc0, c1 = p1 + w[a].sc1;
+            const double p0 = w[a].wa0 + wn0[a], p1 = w[a].wa1 + wn1[a];
+            const double c0 = p0 + w[a].wm0, c1 = p1 + w[a].wm1;
 #if MM_SHIFT_LDS
             const double left = lds_shift(c1, c.from_lower);
             const double right = lds_shift(c0, c.from_upper);
 #else
-            const double left = dpp_lower(c1);   // c3 at column y0-1 (lane-1's second column)
-            const double right = dpp_upper(c0);  // c3 at column y0+2 (lane+1's first column)
+            const double left = dpp_lower(c1);   // cw at column y0-1 (lane-1's second column)
+            const double right = dpp_upper(c0);  // cw at column y0+2 (lane+1's first column)
 #endif
-            w0[a] = w[a].dc0 + ((left + c1) + p0);
-            w1[a] = w[a].dc1 + ((c0 + right) + p1);
+            const double r8 = A.drate[a] * 0.125;
+            o0[a] = __builtin_fma(__builtin_fma(w[a].um0, m0, (left + c1) + p0), r8, w[a].um0);
+            o1[a] = __builtin_fma(__builtin_fma(w[a].um1, m1, (c0 + right) + p1), r8, w[a].um1);
         }
-        w[a].sp0 = w[a].sc0;
-        w[a].sp1 = w[a].sc1;
-        w[a].sc0 = sn0[a];
-        w[a].sc1 = sn1[a];
-        w[a].dc0 = dn0[a];
-        w[a].dc1 = dn1[a];
+        w[a].wa0 = w[a].wm0;
+        w[a].wa1 = w[a].wm1;
+        w[a].wm0 = wn0[a];
+        w[a].wm1 = wn1[a];
+        w[a].um0 = u0[a];
+        w[a].um1 = u1[a];
     }
     if (CHAIN && A.npost) {
-        chain_k<NA>(w0, A.npost, A.post_a, A.post_b, A.post_r);
-        chain_k<NA>(w1, A.npost, A.post_a, A.post_b, A.post_r);
+        chain_k<NA>(o0, A.npost, A.post_a, A.post_b, A.post_r);
+        chain_k<NA>(o1, A.npost, A.post_a, A.post_b, A.post_r);
     }
 }
 

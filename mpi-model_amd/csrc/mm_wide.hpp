@@ -2,9 +2,11 @@
 // flow): K fused steps per HBM pass, the K levels spread over the P waves of a workgroup.
 //
 // The step is the generalisation of src/Model.hpp:176-235 + src/Exponencial.hpp:18-20 to
-// every cell (oracle/mm_oracle.h): per cell out = r*u, s = out/cnt, d = u - out and
-// v' = d + ((c3(y-1) + c3(y+1)) + p), p = s(x-1) + s(x+1), c3 = p + s(x). Every level below
-// is that single step, so K fused levels are bit-identical to K single steps.
+// every cell (oracle/mm_oracle.h): per cell the neighbours' weights w = u * 8/cnt (w = u
+// where cnt = 8, 0 outside the grid), pw = w(x-1) + w(x+1), cw = pw + w(x),
+// W8 = (cw(y-1) + cw(y+1)) + pw and v' = fma(fma(u, -8, W8), r/8, u) -- the out = r*u,
+// share = out/cnt of every neighbour with r/8 factored out of the sum. Every level below is
+// that single step, so K fused levels are bit-identical to K single steps.
 //
 // Why split the levels. A K-level pipeline keeps, per level and column, the shares of two
 // rows and the kept value of one (three doubles) plus the row handed to the next level.
@@ -107,9 +109,7 @@ enum { kBodyFast = 0, kBodyEdge = 1, kBodyGen = 2 };
 template <int C>
 struct WLane {
     long long H;
-    int sy[C];      // column spans of this lane's columns
-    int cnt[C];     // neighbour counts of the columns in an interior row (8 / 5 / 0 ...)
-    bool special;   // some column of this lane has cnt != 8 (edge strips only)
+    int sy[C];      // column spans of this lane's columns (cnt = row span * sy - 1)
     bool eL, eR;    // EDGE body: this lane holds the grid's first column as its column 0 /
                     // its last column as its column C-1
     bool gen;       // (wave-uniform) a strip the EDGE body cannot run: every group GEN
@@ -117,107 +117,100 @@ struct WLane {
     double ownw[C]; // own as 1.0 / 0.0 (RED: the weights of the all-rows-owned groups)
 };
 
-// One level's window, per column: shares of the row above (sp), shares and u - out of the
-// current row (sc, dc).
+// One level's window, per column: the weights w of the row above (wa) and of the current
+// row (wm), and the current row's values (um). FAST rows hold no wm: there w = u, so the
+// window is (wa, um) and wm is rebuilt from um when a FAST run of groups ends (wave_run).
 template <int C>
 struct WinC {
-    double sp[C], sc[C], dc[C];
+    double wa[C], wm[C], um[C];
 };
 
-// s and d of this lane's columns of row gx (oracle/mm_oracle.c emit). FAST: interior
-// row of an interior strip (cnt == 8: s = u*(r/8), d = fma(s, -8, u)). EDGE: interior row
-// of a strip holding the grid's first (or last) column as a lane's column 0 (C-1), the
-// columns past it in whole lanes: every lane divides that column's out by its 5
-// neighbours, the lane holding it keeps the result -- no branch (the branches of the
-// per-lane fix-up below cost the edge strips 3.7x the rows' time, round 5); the columns
-// past the grid compute anything, and wemit keeps it from crossing into the grid. GEN:
-// any row and strip (the row class is wave-uniform; lanes redo their columns whose count
-// is not 8).
+// 8/cnt for the neighbour counts a cell can have (oracle/mm_oracle.c c8_of): the same
+// correctly rounded quotients, no division at run time
+__device__ __forceinline__ double c8_of(int cnt) {
+    return cnt == 8 ? 1.0
+                    : (cnt == 5 ? 8.0 / 5.0
+                                : (cnt == 3 ? 8.0 / 3.0
+                                            : (cnt == 2 ? 4.0 : (cnt == 1 ? 8.0 : 0.0))));
+}
+
+// The weights w of this lane's columns of row gx (oracle/mm_oracle.c w_row). FAST:
+// interior row of an interior strip, w = u. EDGE: interior row of a strip holding the
+// grid's first (or last) column as a lane's column 0 (C-1), the columns past it in whole
+// lanes: the lane holding it scales that column by 8/5 (a multiply every lane issues, a
+// select) -- no branch; the columns past the grid keep w = u, and wemit keeps them from
+// crossing into the grid. GEN: any row and strip (the row class is wave-uniform): every
+// column by its own count, 0 outside the grid.
 template <int C, int BODY>
-__device__ __forceinline__ void procc(const WLane<C>& c, double r, double r8, long long gx,
-                                      const double (&u)[C], double (&s)[C], double (&d)[C]) {
-    const int sx = BODY == kBodyGen ? span3k(c.H, gx) : 3;
-    if (sx == 3) {
+__device__ __forceinline__ void procc(const WLane<C>& c, long long gx, const double (&u)[C],
+                                      double (&w)[C]) {
 #pragma unroll
-        for (int k = 0; k < C; ++k) {
-            s[k] = u[k] * r8;
-            d[k] = __builtin_fma(s[k], -8.0, u[k]);
-        }
-        if (BODY == kBodyEdge) {
-            const double us = c.eL ? u[0] : u[C - 1];
-            const double out = r * us;
-            const double sd = out / 5.0;  // oracle emit: cnt 5, s = out / cnt, d = u - out
-            const double dd = us - out;
-            s[0] = c.eL ? sd : s[0];
-            d[0] = c.eL ? dd : d[0];
-            s[C - 1] = c.eR ? sd : s[C - 1];
-            d[C - 1] = c.eR ? dd : d[C - 1];
-        } else if (BODY == kBodyGen && c.special) {
+    for (int k = 0; k < C; ++k) w[k] = u[k];
+    if (BODY == kBodyEdge) {
+        constexpr double k85 = 8.0 / 5.0;
+        const double w0 = u[0] * k85, w1 = u[C - 1] * k85;
+        w[0] = c.eL ? w0 : w[0];
+        w[C - 1] = c.eR ? w1 : w[C - 1];
+    } else if (BODY == kBodyGen) {
+        const int sx = span3k(c.H, gx);
 #pragma unroll
-            for (int k = 0; k < C; ++k)
-                if (c.cnt[k] != 8) emit_k(r, u[k], c.cnt[k], s[k], d[k]);
-        }
-    } else if (sx == 0) {  // row outside the grid: emits nothing
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            s[k] = 0.0;
-            d[k] = u[k];
-        }
-    } else {  // the grid's first / last row: 5 / 3 neighbours
-#pragma unroll
-        for (int k = 0; k < C; ++k) emit_k(r, u[k], c.sy[k] ? sx * c.sy[k] - 1 : 0, s[k], d[k]);
+        for (int k = 0; k < C; ++k) w[k] = u[k] * c8_of(sx * c.sy[k] - 1);
     }
 }
 
 // Level input m = 0 / 1 (row gx): fill the window.
 template <int C, int BODY>
-__device__ __forceinline__ void wfill(const WLane<C>& c, double r, double r8, long long gx, int m,
-                                      WinC<C>& w, const double (&u)[C]) {
-    double s[C], d[C];
-    procc<C, BODY>(c, r, r8, gx, u, s, d);
+__device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, WinC<C>& win,
+                                      const double (&u)[C]) {
+    double w[C];
+    procc<C, BODY>(c, gx, u, w);
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         if (m == 0) {
-            w.sp[k] = s[k];
+            win.wa[k] = w[k];
         } else {
-            w.sc[k] = s[k];
-            w.dc[k] = d[k];
+            win.wm[k] = w[k];
+            win.um[k] = u[k];
         }
     }
 }
 
-// Level input m >= 2 (row gx): emit the window's current row, slide the window.
+// Level input m >= 2 (row gx): emit the window's current row (gx - 1), slide the window.
 template <int C, int BODY>
-__device__ __forceinline__ void wemit(const WLane<C>& c, double r, double r8, long long gx,
-                                      WinC<C>& w, const double (&u)[C], double (&o)[C]) {
-    double sn[C], dn[C];
-    procc<C, BODY>(c, r, r8, gx, u, sn, dn);
-    double p[C], c3[C];
+__device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx, WinC<C>& win,
+                                      const double (&u)[C], double (&o)[C]) {
+    double wn[C];
+    procc<C, BODY>(c, gx, u, wn);
+    double pw[C], cw[C];
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        p[k] = w.sp[k] + sn[k];
-        c3[k] = p[k] + w.sc[k];
+        pw[k] = win.wa[k] + wn[k];
+        cw[k] = pw[k] + (BODY == kBodyFast ? win.um[k] : win.wm[k]);
     }
-    double left = dpp_lower(c3[C - 1]);  // c3 of column y0-1 (lane-1's last column)
-    double right = dpp_upper(c3[0]);     // c3 of column y0+C (lane+1's first column)
+    double left = dpp_lower(cw[C - 1]);  // cw of column y0-1 (lane-1's last column)
+    double right = dpp_upper(cw[0]);     // cw of column y0+C (lane+1's first column)
     if (BODY != kBodyFast) {
-        // outside the grid s = 0, so c3 = 0 there: EDGE rows compute anything in the lanes
-        // past the grid (procc), and GEN rows of the same strip still hold such shares in
+        // outside the grid w = 0, so cw = 0 there: EDGE rows compute anything in the lanes
+        // past the grid (procc), and GEN rows of the same strip still hold such weights in
         // their windows from the EDGE rows before them
         left = c.eL ? 0.0 : left;
         right = c.eR ? 0.0 : right;
     }
+    // a cell without neighbours (a 1 x 1 grid) keeps its value: m8 = 0
+    const int sxm = BODY == kBodyGen ? span3k(c.H, gx - 1) : 3;
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        const double cl = k == 0 ? left : c3[k - 1];
-        const double cr = k == C - 1 ? right : c3[k + 1];
-        o[k] = w.dc[k] + ((cl + cr) + p[k]);
+        const double cl = k == 0 ? left : cw[k - 1];
+        const double cr = k == C - 1 ? right : cw[k + 1];
+        const double m8 = (BODY == kBodyGen && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
+        const double t = __builtin_fma(win.um[k], m8, (cl + cr) + pw[k]);
+        o[k] = __builtin_fma(t, r8, win.um[k]);
     }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        w.sp[k] = w.sc[k];
-        w.sc[k] = sn[k];
-        w.dc[k] = dn[k];
+        win.wa[k] = BODY == kBodyFast ? win.um[k] : win.wm[k];
+        if (BODY != kBodyFast) win.wm[k] = wn[k];
+        win.um[k] = u[k];
     }
 }
 
@@ -265,7 +258,7 @@ struct WCtx {
     int start;            // first iteration of this wave (p * D)
     int dmask;            // bit a: attribute a diffuses (NA > 1)
     long long g0;         // global row of input row 0 (rA - K)
-    double r[NA], r8[NA];
+    double r8[NA];        // rate / 8 of each attribute
     unsigned voff, soff, rowb;
     __amdgpu_buffer_rsrc_t in[NA], out[NA];
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
@@ -421,14 +414,14 @@ __device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 if (m == 0) {
-                    w[a].sp[k] = 0.0;
+                    w[a].wa[k] = 0.0;
                 } else {
-                    w[a].sc[k] = 0.0;
-                    w[a].dc[k] = u[a][k];
+                    w[a].wm[k] = 0.0;
+                    w[a].um[k] = u[a][k];
                 }
             }
         } else {
-            wfill<C, BODY>(x.c, x.r[a], x.r8[a], gx, m, w[a], u[a]);
+            wfill<C, BODY>(x.c, gx, m, w[a], u[a]);
         }
     }
 }
@@ -444,13 +437,13 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
         if (NA > 1 && !((x.dmask >> a) & 1)) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                o[a][k] = w[a].dc[k];
-                w[a].sp[k] = w[a].sc[k];
-                w[a].sc[k] = 0.0;
-                w[a].dc[k] = u[a][k];
+                o[a][k] = w[a].um[k];
+                w[a].wa[k] = 0.0;
+                w[a].wm[k] = 0.0;
+                w[a].um[k] = u[a][k];
             }
         } else {
-            wemit<C, BODY>(x.c, x.r[a], x.r8[a], gx, w[a], u[a], o[a]);
+            wemit<C, BODY>(x.c, x.r8[a], gx, w[a], u[a], o[a]);
         }
     }
     if constexpr (NA > 1 && MM_CHAIN_ASM) {
@@ -611,26 +604,15 @@ __device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, 
     }
 }
 
-// The whole schedule of one wave. MID: body of the groups whose rows are all interior.
-// RED: every level's sum of this wave's owned cells is added to carry[level][attribute]
-// (wave-uniform), so a workgroup that runs several segments sums them all.
-template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
-__device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
-                                         double (&carry)[KW][NA]) {
+// The pipeline fill of one wave (its first input rows, every level joining in turn) up to
+// its first group boundary, on the BODY rows' code; returns the first iteration of the
+// group loop. The first wave loads U rows ahead and starts at iteration 0 (its ring slots
+// compile-time); the others join the barriers until their start.
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int BODY>
+__device__ __forceinline__ int wave_prologue(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st) {
     using G = WGeom<KW, P, B>;
-    constexpr int K = G::K;
-    static_assert(B % U == 0, "ring slots repeat within a group");
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;
-    WState<C, NA, KW, U> st;
-#pragma unroll
-    for (int q = 0; q < KW; ++q) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a) st.acc[q][a] = 0.0;
-    }
-    int s;  // first iteration of the group loop
     if (kIn) {
-        // start = 0: the prologue and the iterations up to the first group boundary are
-        // unrolled (compile-time ring slots)
 #pragma unroll
         for (int k = 0; k < U; ++k) {
 #pragma unroll
@@ -643,29 +625,65 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
 #pragma unroll
         for (int t = 0; t < G::T0; ++t) {
             if (t < G::S0)
-                wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, t, t, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true>(x, st, t, t, t % U);
             else
-                wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, t, 0, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, t, 0, t % U);
             if (P > 1 && (t + 1) % B == 0) wg_sync();
         }
-        s = G::T0;
-    } else {
-        for (int i = 0; i < x.start; ++i) group_end<P, B>(i);
+        return G::T0;
+    }
+    for (int i = 0; i < x.start; ++i) group_end<P, B>(i);
 #pragma unroll
-        for (int t = 0; t < G::S0; ++t) {
-            wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, true>(x, st, x.start + t, t, 0);
-            group_end<P, B>(x.start + t);
-        }
-        s = x.start + G::S0;
-        for (; s % B != 0; ++s) {
-            wave_iter<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, false>(x, st, s, 0, 0);
-            group_end<P, B>(s);
+    for (int t = 0; t < G::S0; ++t) {
+        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true>(x, st, x.start + t, t, 0);
+        group_end<P, B>(x.start + t);
+    }
+    int s = x.start + G::S0;
+    for (; s % B != 0; ++s) {
+        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, s, 0, 0);
+        group_end<P, B>(s);
+    }
+    return s;
+}
+
+// The whole schedule of one wave. MID: body of the groups whose rows are all interior.
+// RED: every level's sum of this wave's owned cells is added to carry[level][attribute]
+// (wave-uniform), so a workgroup that runs several segments sums them all.
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
+__device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
+                                         double (&carry)[KW][NA]) {
+    using G = WGeom<KW, P, B>;
+    constexpr int K = G::K;
+    static_assert(B % U == 0, "ring slots repeat within a group");
+    WState<C, NA, KW, U> st;
+#pragma unroll
+    for (int q = 0; q < KW; ++q) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) st.acc[q][a] = 0.0;
+    }
+    // the pipeline fill on the MID body where the segment's first input rows are interior
+    // rows (every segment but the grid's first and its thin last ones): on the GEN body it
+    // cost ~4 % of a 2541-row K = 20 segment's time
+    const bool pro_mid =
+        !(MID == kBodyEdge && x.c.gen) && x.g0 >= 2 &&
+        x.g0 + (long long)(G::T0 + (P - 1) * G::D + 2 * K + 2 * B) < x.c.H - 1;
+    const int s = pro_mid ? wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, MID>(x, st)
+                          : wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, kBodyGen>(x, st);
+    if (MID == kBodyFast && pro_mid) {  // FAST rows hold no wm (w = u): GEN groups may follow
+#pragma unroll
+        for (int q = 0; q < KW; ++q) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                for (int k = 0; k < C; ++k) st.win[q][a].wm[k] = st.win[q][a].um[k];
+            }
         }
     }
-    // groups whose levels all read interior rows: level j reads row g0 + (j-1) + m,
-    // m = i - start - kSkew*q, i.e. rows g0 + p*KW + (i - start) - (kSkew-1)q, q < KW
+    // groups whose levels all read interior rows and emit from interior rows: level j
+    // reads row g0 + (j-1) + m, m = i - start - kSkew*q, i.e. rows g0 + p*KW + (i - start) -
+    // (kSkew-1)q, q < KW, and emits the row before it (FAST takes its w = u)
     const long long base = x.g0 + (long long)x.p * KW - x.start;
-    const long long lo = 1 + (kSkew - 1) * (KW - 1) - base;  // first i with every row >= 1
+    const long long lo = 2 + (kSkew - 1) * (KW - 1) - base;  // first i with every row >= 2
     const long long hi = x.c.H - 1 - base;         // first i with a row > H-2
     long long f0 = lo <= s ? s : s + (lo - s + B - 1) / B * B;
     long long f1 = hi <= s ? s : s + (hi - s) / B * B;
@@ -687,6 +705,16 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
         wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)m1, (int)f1);
     } else {
         wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
+    }
+    if (MID == kBodyFast && f1 > f0) {  // FAST rows hold no wm (w = u there): rebuild it
+#pragma unroll
+        for (int q = 0; q < KW; ++q) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                for (int k = 0; k < C; ++k) st.win[q][a].wm[k] = st.win[q][a].um[k];
+            }
+        }
     }
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
     if (RED) {
@@ -738,12 +766,9 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
     x.soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
     x.rowb = (unsigned)(A.pitch * 8);
     x.c.H = A.H;
-    x.c.special = false;
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         x.c.sy[k] = span3k(W, y0 + k);
-        x.c.cnt[k] = x.c.sy[k] ? 3 * x.c.sy[k] - 1 : 0;
-        x.c.special = x.c.special || x.c.cnt[k] != 8;
         x.c.own[k] = store_lane && y0 + k < W;
         x.c.ownw[k] = x.c.own[k] ? 1.0 : 0.0;
     }
@@ -757,8 +782,7 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
     x.g0 = A.x_init + x.rA - K;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        x.r[a] = A.drate[a];
-        x.r8[a] = x.r[a] * 0.125;
+        x.r8[a] = A.drate[a] * 0.125;
         x.in[a] = rows_rsrc(A.in[a] + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K,
                             A.pitch);
         x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);

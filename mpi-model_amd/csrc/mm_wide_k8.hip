@@ -4,6 +4,13 @@
 // the pipeline fill of the 108-row segments of C2 (4096^2) is 6 iterations shorter per
 // wave, 85.0 / 84.3 vs 87.2 / 86.6 us per 8-step pass in two sweeps; groups of 1 row
 // 101 us; an LDS-DMA input ring 8 / 12 rows deep 86.0 / 86.5 us.
+// Three workgroups per CU (168 VGPRs, `MM_WIDE_MIN_WAVES 3`): with the GEN / EDGE bodies and
+// the MID-body pipeline fill of round 5 the instance took 188 VGPRs, two per CU, and C2
+// fell from 1564 to 1435 GCUPS with longer segments; at 168 the steady loops are
+// unchanged (no scratch, tools/asm_steady.py), the spills sit in the GEN paths.
+#ifndef MM_WIDE_MIN_WAVES
+#define MM_WIDE_MIN_WAVES 3
+#endif
 #ifndef MM_WIDE_U
 #define MM_WIDE_U 2
 #endif

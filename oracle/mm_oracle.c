@@ -93,34 +93,25 @@ void or_point_apply(long long H, long long W, double* v, long long sx, long long
     v[sx * W + sy] = v[sx * W + sy] - out;          /* Model.hpp:211 */
 }
 
-/* One emitter of the whole-grid step: its share s and what it keeps, d = v - out.
- * cnt == 8 (every interior cell): s = v * (rate/8) and d = fma(s, -8, v) -- with
- * out = rate*v these are RN(out)/8 and RN(v - out) exactly (scaling by 2^-3 commutes with
- * rounding and 8*s == RN(out)) whenever out is a normal number, and they save the device
- * kernels one multiply per cell. Other counts: out = rate*v, s = out/cnt, d = v - out. */
-static inline void emit(double rate, double v, int cnt, double* s, double* d) {
-    if (cnt == 8) {
-        *s = v * (rate * 0.125);
-        *d = fma(*s, -8.0, v);
-    } else if (cnt > 0) {
-        double out = rate * v;
-        *s = out / (double)cnt;
-        *d = v - out;
-    } else {
-        *s = 0.0;
-        *d = v;
-    }
+/* The whole-grid step (mm_oracle.h): every emitter's outflow is out = r*v and each of
+ * its cnt neighbours receives out/cnt. Written per receiving cell c with the neighbours'
+ * weights w = v * 8/cnt (w = v for cnt == 8, 0 outside the grid):
+ *   v'(c) = v - r*v + sum_nbr r*v_nbr/cnt_nbr = v + (r/8) * (W8 - 8v),  W8 = sum_nbr w_nbr
+ * computed as fma(fma(v, -8, W8), r/8, v) -- the multiply by r/8 factored out of the sum,
+ * so an interior cell costs no multiply for its neighbours' shares. */
+static inline double c8_of(int cnt) { return cnt == 8 ? 1.0 : (cnt > 0 ? 8.0 / (double)cnt : 0.0); }
+
+static inline double update_of(double v, double w8, int cnt, double r8) {
+    return cnt > 0 ? fma(fma(v, -8.0, w8), r8, v) : v;
 }
 
-/* s row of global row gx (NULL vrow or outside grid -> +0.0) */
-static void s_row(long long H, long long W, long long gx, const double* vrow,
-                  double rate, double* s) {
+/* w row of global row gx (NULL vrow or outside grid -> +0.0) */
+static void w_row(long long H, long long W, long long gx, const double* vrow, double* w) {
     if (vrow == NULL || gx < 0 || gx >= H) {
-        for (long long y = 0; y < W; ++y) s[y] = 0.0;
+        for (long long y = 0; y < W; ++y) w[y] = 0.0;
         return;
     }
-    double d;
-    for (long long y = 0; y < W; ++y) emit(rate, vrow[y], or_neighbor_count(H, W, gx, y), &s[y], &d);
+    for (long long y = 0; y < W; ++y) w[y] = vrow[y] * c8_of(or_neighbor_count(H, W, gx, y));
 }
 
 /* rows(gx) gives the v row for any global gx in [x_lo-1, x_hi]. */
@@ -129,35 +120,34 @@ typedef const double* (*row_fn)(const void* ctx, long long gx);
 static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
                       row_fn rows, const void* ctx, double* vout, double rate) {
     double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
-    double* s_prev = buf;
-    double* s_cur = buf + W;
-    double* s_next = buf + 2 * W;
-    double* p = buf + 3 * W;
-    double* c3 = buf + 4 * W; /* W+2 entries, c3[y+1] for column y */
-    c3[0] = 0.0;
-    c3[W + 1] = 0.0;
-    s_row(H, W, x_lo - 1, rows(ctx, x_lo - 1), rate, s_prev);
-    s_row(H, W, x_lo, rows(ctx, x_lo), rate, s_cur);
+    double* w_prev = buf;
+    double* w_cur = buf + W;
+    double* w_next = buf + 2 * W;
+    double* pw = buf + 3 * W;
+    double* cw = buf + 4 * W; /* W+2 entries, cw[y+1] for column y */
+    const double r8 = rate * 0.125;
+    cw[0] = 0.0;
+    cw[W + 1] = 0.0;
+    w_row(H, W, x_lo - 1, rows(ctx, x_lo - 1), w_prev);
+    w_row(H, W, x_lo, rows(ctx, x_lo), w_cur);
     for (long long x = x_lo; x < x_hi; ++x) {
-        s_row(H, W, x + 1, rows(ctx, x + 1), rate, s_next);
+        w_row(H, W, x + 1, rows(ctx, x + 1), w_next);
         for (long long y = 0; y < W; ++y) {
-            p[y] = s_prev[y] + s_next[y];
-            c3[y + 1] = p[y] + s_cur[y];
+            pw[y] = w_prev[y] + w_next[y];
+            cw[y + 1] = pw[y] + w_cur[y];
         }
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
         if (v == NULL) {  /* output row outside the grid (or the slab): no cells, zeros */
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
         } else for (long long y = 0; y < W; ++y) {
-            double sy, d;
-            emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
-            double nb = (c3[y] + c3[y + 2]) + p[y];
-            o[y] = d + nb;
+            const double w8 = (cw[y] + cw[y + 2]) + pw[y];
+            o[y] = update_of(v[y], w8, or_neighbor_count(H, W, x, y), r8);
         }
-        double* t = s_prev;
-        s_prev = s_cur;
-        s_cur = s_next;
-        s_next = t;
+        double* t = w_prev;
+        w_prev = w_cur;
+        w_cur = w_next;
+        w_next = t;
     }
     free(buf);
 }
@@ -192,17 +182,15 @@ void or_field_step_slab(long long H, long long W, long long x_init, long long h,
 #else
 #define OR_FAST_TARGET
 #endif
-static OR_FAST_TARGET void s_row_fast(long long H, long long W, long long gx,
-                                      const double* vrow, double rate, double* s) {
-    if (vrow == NULL || gx < 0 || gx >= H || gx == 0 || gx == H - 1 || W < 3) {
-        s_row(H, W, gx, vrow, rate, s);
+static OR_FAST_TARGET void w_row_fast(long long H, long long W, long long gx,
+                                      const double* vrow, double* w) {
+    if (vrow == NULL || gx <= 0 || gx >= H - 1 || W < 3) {
+        w_row(H, W, gx, vrow, w);
         return;
     }
-    const double r8 = rate * 0.125;
-    double d;
-    emit(rate, vrow[0], or_neighbor_count(H, W, gx, 0), &s[0], &d);
-    for (long long y = 1; y < W - 1; ++y) s[y] = vrow[y] * r8;
-    emit(rate, vrow[W - 1], or_neighbor_count(H, W, gx, W - 1), &s[W - 1], &d);
+    w[0] = vrow[0] * c8_of(or_neighbor_count(H, W, gx, 0));
+    for (long long y = 1; y < W - 1; ++y) w[y] = vrow[y];  /* cnt 8: w = v * 1.0 = v */
+    w[W - 1] = vrow[W - 1] * c8_of(or_neighbor_count(H, W, gx, W - 1));
 }
 
 static OR_FAST_TARGET void step_rows_fast(long long H, long long W, long long x_lo,
@@ -210,47 +198,39 @@ static OR_FAST_TARGET void step_rows_fast(long long H, long long W, long long x_
                                           double* vout, double rate) {
     double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
     if (!buf) return;
-    double* s_prev = buf;
-    double* s_cur = buf + W;
-    double* s_next = buf + 2 * W;
-    double* p = buf + 3 * W;
-    double* c3 = buf + 4 * W;
-    c3[0] = 0.0;
-    c3[W + 1] = 0.0;
-    s_row_fast(H, W, x_lo - 1, rows(ctx, x_lo - 1), rate, s_prev);
-    s_row_fast(H, W, x_lo, rows(ctx, x_lo), rate, s_cur);
+    double* w_prev = buf;
+    double* w_cur = buf + W;
+    double* w_next = buf + 2 * W;
+    double* pw = buf + 3 * W;
+    double* cw = buf + 4 * W;
+    const double r8 = rate * 0.125;
+    cw[0] = 0.0;
+    cw[W + 1] = 0.0;
+    w_row_fast(H, W, x_lo - 1, rows(ctx, x_lo - 1), w_prev);
+    w_row_fast(H, W, x_lo, rows(ctx, x_lo), w_cur);
     for (long long x = x_lo; x < x_hi; ++x) {
-        s_row_fast(H, W, x + 1, rows(ctx, x + 1), rate, s_next);
+        w_row_fast(H, W, x + 1, rows(ctx, x + 1), w_next);
         for (long long y = 0; y < W; ++y) {
-            p[y] = s_prev[y] + s_next[y];
-            c3[y + 1] = p[y] + s_cur[y];
+            pw[y] = w_prev[y] + w_next[y];
+            cw[y + 1] = pw[y] + w_cur[y];
         }
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
         if (v == NULL) {
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
         } else if (x > 0 && x < H - 1 && W >= 3) {
-            for (long long y = 0; y < W; y += W - 1) {  /* first and last column */
-                double sy, d;
-                emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
-                o[y] = d + ((c3[y] + c3[y + 2]) + p[y]);
-            }
-            for (long long y = 1; y < W - 1; ++y) {  /* cnt == 8: d = fma(s, -8, v) */
-                double d = fma(s_cur[y], -8.0, v[y]);
-                double nb = (c3[y] + c3[y + 2]) + p[y];
-                o[y] = d + nb;
-            }
+            for (long long y = 0; y < W; y += W - 1)  /* first and last column */
+                o[y] = update_of(v[y], (cw[y] + cw[y + 2]) + pw[y], or_neighbor_count(H, W, x, y), r8);
+            for (long long y = 1; y < W - 1; ++y)  /* cnt == 8 */
+                o[y] = fma(fma(v[y], -8.0, (cw[y] + cw[y + 2]) + pw[y]), r8, v[y]);
         } else {
-            for (long long y = 0; y < W; ++y) {
-                double sy, d;
-                emit(rate, v[y], or_neighbor_count(H, W, x, y), &sy, &d);
-                o[y] = d + ((c3[y] + c3[y + 2]) + p[y]);
-            }
+            for (long long y = 0; y < W; ++y)
+                o[y] = update_of(v[y], (cw[y] + cw[y + 2]) + pw[y], or_neighbor_count(H, W, x, y), r8);
         }
-        double* t = s_prev;
-        s_prev = s_cur;
-        s_cur = s_next;
-        s_next = t;
+        double* t = w_prev;
+        w_prev = w_cur;
+        w_cur = w_next;
+        w_next = t;
     }
     free(buf);
 }

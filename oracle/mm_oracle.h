@@ -9,23 +9,26 @@
  * against golden grids produced by the reference itself (tests/golden/, made by
  * tests/golden/make_golden.py from oracle/_ref/). The generalised whole-grid,
  * multi-step step (or_field_step*) has no reference implementation (the
- * reference's time loop is commented out, Model.hpp:180-183); it is pinned
- * through the single-source case (rate zero everywhere but the source reduces
- * it to Model.hpp:176-235 bit-for-bit) plus invariants (conservation, flip
- * symmetry, uniform fixed point). See DESIGN.md section "Oracle".
+ * reference's time loop is commented out, Model.hpp:180-183). It is pinned to the
+ * reference's arithmetic through or_field_step_general, which applies the reference's
+ * update (Model.hpp:176-235: out = r*v, share = out/cnt, neighbours += share, source -=
+ * out) to an arbitrary outflow field and is bit-for-bit the reference's single-source
+ * application when the outflow is zero but at the source; with out = r*v everywhere it
+ * equals or_field_step within a few ulp (tests/test_oracle.py: 1e-14 relative), plus
+ * invariants (conservation, flip symmetry, uniform fixed point). See DESIGN.md "Oracle".
  *
- * Arithmetic contract (shared with the HIP kernels, compiled -ffp-contract=off):
- *   out(c) = r * v(c)                                   Exponencial.hpp:18-20
- *   s(c)   = out(c) / cnt(c)                            Model.hpp:199
- *   d(c)   = v(c) - out(c)                              Model.hpp:211
- *   p(c)   = s(x-1,y) + s(x+1,y)
- *   c3(c)  = p(c) + s(c)
- *   nb(c)  = (c3(x,y-1) + c3(x,y+1)) + p(c)
- *   v'(c)  = d(c) + nb(c)                               Model.hpp:206-211,234
- * computed for cnt == 8 as s = v*(r*0.125), d = fma(s, -8, v) -- the same two numbers
- * whenever r*v is normal (2^-3 scaling is exact), one multiply fewer per cell.
- * s is +0.0 outside the global grid; cnt is the number of in-grid Moore
- * neighbours (Cell.hpp:71-157 gives 3/5/8 for grids of at least 2x2).
+ * Arithmetic contract of the whole-grid step (shared with the HIP kernels, compiled
+ * -ffp-contract=off, the two fma explicit):
+ *   w(c)  = v(c) * c8(c),  c8 = 8/cnt(c) rounded (1 for cnt 8: w = v), 0 outside the grid
+ *   pw(c) = w(x-1,y) + w(x+1,y)
+ *   cw(c) = pw(c) + w(c)
+ *   W8(c) = (cw(x,y-1) + cw(x,y+1)) + pw(c)
+ *   v'(c) = fma(fma(v(c), -8, W8(c)), r/8, v(c))        (cnt(c) > 0; else v' = v)
+ * i.e. v' = v - r*v + sum_nbr r*v_nbr/cnt_nbr (Exponencial.hpp:18-20: out = r*v;
+ * Model.hpp:199: share = out/cnt; Model.hpp:206-211,234: neighbours += share, source
+ * -= out) with r/8 factored out of the neighbours' sum: an interior cell's neighbours
+ * cost no multiply. cnt is the number of in-grid Moore neighbours (Cell.hpp:71-157 gives
+ * 3/5/8 for grids of at least 2x2).
  */
 #ifndef MM_ORACLE_H
 #define MM_ORACLE_H

@@ -8,7 +8,7 @@
  * Exercises every function of mm_oracle.h on small and degenerate grids (1x1, 1xW, Hx1,
  * 2x2, ragged) and checks the invariants that need no reference: the slab decomposition
  * reproduces the whole-grid step bit for bit, the step conserves the total, the general
- * step with out = r*v is the step, the flow program conserves its attributes' total.
+ * step with out = r*v is the step to a few ulp, the flow program conserves its attributes' total.
  * Exit status 0 = all checks passed and no sanitizer report.
  */
 #include <math.h>
@@ -40,13 +40,14 @@ static void grid_case(long long H, long long W) {
     /* conservation */
     const double s0 = or_sum(v, n), s1 = or_sum(a, n);
     CHECK(fabs(s1 - s0) <= 1e-12 * s0, "conservation %lldx%lld", H, W);
-    /* general step with out = r*v for every cell that has neighbours: equal to the step
-     * (the interior form s = v*(r/8), d = fma(s, -8, v) gives the same numbers) */
+    /* general step with out = r*v for every cell that has neighbours: the step's value up
+     * to rounding (the step factors r/8 out of the neighbours' sum) */
     for (long long x = 0; x < H; ++x)
         for (long long y = 0; y < W; ++y)
             outf[x * W + y] = or_neighbor_count(H, W, x, y) > 0 ? 0.3 * v[x * W + y] : 0.0;
     or_field_step_general(H, W, v, outf, b);
-    for (size_t i = 0; i < n; ++i) CHECK(a[i] == b[i], "general %lldx%lld at %zu", H, W, i);
+    for (size_t i = 0; i < n; ++i)
+        CHECK(fabs(a[i] - b[i]) <= 1e-14 * fabs(b[i]), "general %lldx%lld at %zu", H, W, i);
     /* slab decomposition: every G, ghost rows from the neighbours */
     for (int G = 1; G <= 4 && G <= H; ++G) {
         for (int g = 0; g < G; ++g) {

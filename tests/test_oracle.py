@@ -57,7 +57,11 @@ def test_uniform_rate_step_equals_general_form(O, shape):
     # a cell without neighbours (1x1 grid) cannot emit: its outflow is 0
     emits = np.array([[O.neighbor_count(H, W, x, y) > 0 for y in range(W)] for x in range(H)])
     outf = np.where(emits, 0.1 * v, 0.0)
-    assert np.array_equal(O.field_step(v, 0.1), O.field_step_general(v, outf))
+    # the reference's update written per emitter (shares) against the whole-grid step's
+    # per-receiver form (r/8 factored out of the neighbours' weights): the same sum,
+    # rounded differently -- a few ulp (mm_oracle.h)
+    got, want = O.field_step(v, 0.1), O.field_step_general(v, outf)
+    assert np.max(np.abs(got - want) / np.abs(want)) <= 1e-14
 
 
 def test_step_count_matches_reference_loop(O):
