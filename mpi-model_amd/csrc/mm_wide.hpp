@@ -93,6 +93,9 @@ namespace {
 #ifndef MM_WIDE_MIN_WAVES
 #define MM_WIDE_MIN_WAVES 2  // __launch_bounds__ waves per SIMD of the C = 4 instances
 #endif
+#ifndef MM_WIDE_PRO_MID
+#define MM_WIDE_PRO_MID 1  // 0: the pipeline fill of every segment on the GEN body
+#endif
 #ifndef MM_WIDE_ASC
 #define MM_WIDE_ASC 0  // 1: levels in ascending order, each consuming the level below's row
 #endif                 // of the same iteration (no pend registers; skew 2 instead of 3)
@@ -665,7 +668,7 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
     // rows (every segment but the grid's first and its thin last ones): on the GEN body it
     // cost ~4 % of a 2541-row K = 20 segment's time
     const bool pro_mid =
-        !(MID == kBodyEdge && x.c.gen) && x.g0 >= 2 &&
+        MM_WIDE_PRO_MID && !(MID == kBodyEdge && x.c.gen) && x.g0 >= 2 &&
         x.g0 + (long long)(G::T0 + (P - 1) * G::D + 2 * K + 2 * B) < x.c.H - 1;
     const int s = pro_mid ? wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, MID>(x, st)
                           : wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, kBodyGen>(x, st);
