@@ -194,10 +194,7 @@ int mm_device_synchronize(int device);
  * kernel; fixes K), MM_PASS_PLAN=0
  * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
  * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP and MM_KERNEL_VARIANT (non-temporal stores;
- * the four-attribute K = 8 instances always store non-temporal) override tuning; MM_LIN=0/1
- * turns the wide kernel's linear plan (one round of workgroups sharing a pass; auto on
- * one-attribute passes with >= 24 K rows per workgroup, not with MM_SEG_WAVES) off / on,
- * MM_LIN_WORKERS / MM_LIN_MAXR set its workgroups / segment length (tests);
+ * the four-attribute K = 8 instances always store non-temporal) override tuning;
  * MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
  * path, result unchanged).

@@ -109,11 +109,6 @@ struct mm_engine {
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
     double seg_edge = 0.0;   // edge-strip segment length / interior length (MM_SEG_EDGE; 0: auto)
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP, mm_passk_kernel)
-    int lin = 0;             // mm_wide_kernel linear plan (MM_LIN=1 on; -1 auto, wide_lin: off
-                             // by default until it beats the segment plan)
-    int lin_workers = 0;     // linear plan: workgroups (MM_LIN_WORKERS; 0: the resident slots)
-    int lin_maxr = 0;        // linear plan: rows per segment at most (MM_LIN_MAXR; 0: offset bound)
-    long long lin_reserve = -1;  // linear plan: slots left to a split pass's border (MM_LIN_RESERVE)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
     std::map<long long, int> bpc;  // wide kernel blocks/CU cache: (variant, red, k)
@@ -565,74 +560,13 @@ long long nstrips_wide(const mm_engine* e, int k) {
     return (e->d.W + oc - 1) / oc;
 }
 
-// Linear plan of rows [lo, hi) for the wide kernel (mm_wide.hpp lin_cost): one round of
-// workgroups, as many as the chip holds at once (the kernel's blocks per CU x CUs), each
-// taking an equal share of the range's cost -- its rows in one strip or the tail of one and
-// the head of the next -- with the edge strips' rows at 1 / seg_edge the cost of the
-// others'. Auto (MM_LIN unset, no MM_SEG_WAVES): one attribute, at least 24 K rows per workgroup, so the
-// pipeline fill of a workgroup's (at most two, plus offset-bound splits) segments stays
-// small against its rows. Returns false where the segment plan runs instead.
-bool wide_lin(mm_engine* e, int k, long long slots, double edge, mm::PassArgs& A,
-              long long lo, long long hi, long long border_blocks) {
-    const long long n = hi - lo, ns = A.nstrips;
-    if (e->lin == 0 || n <= 0 || ns <= 0) return false;
-    const int e2 = std::max(2, (int)std::lround(2.0 / edge));
-    const double rows_eq = (double)n * (ns >= 2 ? (double)(ns - 2) + e2 / 2.0 : e2 / 2.0);
-    // The interior of a split pass leaves slots to the border launch beside it (its blocks
-    // arrive after the exchange; with every slot taken they would run after the interior):
-    // as many as take its rows -- a K-row segment each, plus the pipeline fill (~3K) -- in
-    // the interior's time. MM_LIN_RESERVE overrides.
-    long long reserve = 0;
-    if (border_blocks > 0) {
-        const double per = rows_eq / (double)slots + 3.0 * k;
-        reserve = (long long)std::ceil((double)border_blocks * 4.0 * k / per);
-        reserve = std::min(reserve, slots / 4);
-    }
-    if (e->lin_reserve >= 0 && border_blocks > 0) reserve = std::min(e->lin_reserve, slots - 1);
-    long long workers = e->lin_workers > 0 ? e->lin_workers : slots - reserve;
-    if (e->lin < 0) {
-        if (e->seg_waves > 0.0 || e->na != 1 || rows_eq / (double)slots < 24.0 * k) return false;
-    } else if (e->lin_workers <= 0) {
-        // forced on a small range: a workgroup per 3K rows at least
-        workers = std::min<long long>(slots, std::max<long long>(1, (long long)(rows_eq / (3.0 * k))));
-    }
-    workers = std::max<long long>(1, std::min<long long>(workers, n * ns));
-    const long long maxr = std::max<long long>(1, mm::passk_max_rows(k, e->pitch));
-    A.seg = 1;
-    A.lin = 1;
-    A.lin_e2 = e2;
-    A.lin_maxr = (int)(e->lin_maxr > 0 ? std::min<long long>(e->lin_maxr, maxr) : maxr);
-    A.ra0 = (int)lo;
-    A.ra1 = (int)hi;
-    // every workgroup's segments fit the kernel's list (kLinSegs): more workgroups while
-    // one does not (a range shorter than a workgroup's share of rows, or short MM_LIN_MAXR)
-    for (;;) {
-        A.waves_total = workers;
-        int most = 0;
-        for (long long b = 0; b < workers; ++b)
-            most = std::max(most, mm::lin_segments(A, b, nullptr, 0));
-        if (most <= mm::kLinSegs) break;
-        if (workers >= n * ns) {
-            A.lin = 0;
-            return false;
-        }
-        workers = std::min(n * ns, workers * 2);
-    }
-    A.th = (int)std::max<long long>(1, (long long)(rows_eq / (double)workers));  // rows per workgroup (info)
-    A.th_edge = A.th;
-    A.rb0 = A.rb1 = 0;
-    A.waves_a = A.waves_total = workers;
-    return true;
-}
-
 // Segment plan of rows [lo, hi) for the wide kernel: one workgroup per strip segment, r
 // rows per interior-strip segment and re per edge-strip segment, the smallest r for which
 // the blocks fit seg_waves x the chip's resident blocks. Auto: 4 per resident slot, halved
 // (down to 1) while segments are shorter than 24 K rows -- a segment pays 3K - 1 pipeline
 // iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
-// profiles/r03/kernel_table). Large ranges take the linear plan instead (wide_lin).
-void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi,
-                long long border_blocks = 0) {
+// profiles/r03/kernel_table).
+void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
     const int nt = (e->variant & 1) | wvar(e);
     const int c = wcols(e, k);
     int& bpc = e->bpc[((long long)nt << 8) | (red ? 128 : 0) | k];
@@ -640,8 +574,6 @@ void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lo
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
-    A.lin = 0;
-    if (wide_lin(e, k, (long long)e->ncu * bpc, edge, A, lo, hi, border_blocks)) return;
     const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
     auto re_of = [&](long long rr) {
         return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
@@ -686,10 +618,9 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     long long total_blocks = 0;  // partials units: one per workgroup
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(split_begin(e, depth));
-        wide_range(e, k, red, A, depth, h - depth, 2 * seg_wave_count(depth, A.nstrips, depth, depth));
+        wide_range(e, k, red, A, depth, h - depth);
         const long long interior = A.waves_total;
         mm::PassArgs B = A;
-        B.lin = 0;
         B.th = B.th_edge = depth;
         B.ra0 = 0;
         B.ra1 = depth;
@@ -1203,10 +1134,6 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     if (const char* f = std::getenv("MM_FUSE")) e->passk = e->passk && std::atoi(f) != 0;
     if (const char* p = std::getenv("MM_PASSK")) e->passk = e->passk && std::atoi(p) != 0;
     if (const char* w = std::getenv("MM_WIDE")) e->wide = std::atoi(w) != 0 ? 1 : 0;
-    if (const char* l = std::getenv("MM_LIN")) e->lin = std::atoi(l) < 0 ? -1 : (std::atoi(l) != 0 ? 1 : 0);
-    if (const char* l = std::getenv("MM_LIN_WORKERS")) e->lin_workers = std::max(0, std::atoi(l));
-    if (const char* l = std::getenv("MM_LIN_MAXR")) e->lin_maxr = std::max(0, std::atoi(l));
-    if (const char* l = std::getenv("MM_LIN_RESERVE")) e->lin_reserve = std::max(0, std::atoi(l));
     if (const char* k = std::getenv("MM_STEPS_PER_PASS")) {
         const int v = std::atoi(k);
         if (v >= 1 && (v <= mm::kMaxSteps || (e->wide != 0 && (mm::wide_has(v, 4, 1) || mm::wide_has(v, 2, 4)))))

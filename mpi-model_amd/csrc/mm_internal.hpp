@@ -45,74 +45,7 @@ struct PassArgs {
     int xcd_remap;          // mm_passk_kernel: XCD-contiguous block order (grid padded to 8)
     int seg;                // mm_passk_kernel: segment schedule (th / th_edge rows per wave)
     int th_edge;            // mm_passk_kernel segments: rows per wave of the two edge strips
-    int lin;                // mm_wide_kernel: linear plan (one round of waves_total workgroups
-                            // sharing range a; mm_wide.hpp lin_cost)
-    int lin_e2;             // linear plan: cost of an edge-strip row (an interior row: 2)
-    int lin_maxr;           // linear plan: rows per segment at most (buffer offsets < 2^31)
 };
-
-// The wide kernel's linear plan (mm_wide.hpp, PassArgs::lin): range a's strips end to end
-// in strip order, every row of an interior strip costing 2 units and of the two edge
-// strips lin_e2; workgroup b takes the rows whose cost offset lies in
-// [b*T/n, (b+1)*T/n), n = waves_total, as at most kLinSegs segments of at most lin_maxr
-// rows (the engine checks every workgroup's count with lin_segments).
-constexpr int kLinSegs = 4;
-
-__host__ __device__ inline long long lin_cost(const PassArgs& A) {
-    const long long n = A.ra1 - A.ra0, ns = A.nstrips;
-    return ns >= 2 ? (2LL * A.lin_e2 + 2LL * (ns - 2)) * n : (long long)A.lin_e2 * n;
-}
-
-// strip of cost offset c, its first cost offset and its cost per row
-__host__ __device__ inline void lin_strip(const PassArgs& A, long long c, int& strip,
-                                          long long& base, int& w) {
-    const long long n = A.ra1 - A.ra0, ns = A.nstrips, e = (long long)A.lin_e2 * n;
-    if (ns == 1 || c < e) {
-        strip = 0;
-        base = 0;
-        w = A.lin_e2;
-        return;
-    }
-    const long long s = 1 + (c - e) / (2 * n);
-    if (s >= ns - 1) {
-        strip = (int)(ns - 1);
-        base = e + (ns - 2) * 2 * n;
-        w = A.lin_e2;
-    } else {
-        strip = (int)s;
-        base = e + (s - 1) * 2 * n;
-        w = 2;
-    }
-}
-
-// Segments (strip, first row, end row; local rows) of workgroup blk under the linear plan,
-// at most cap of them written to seg; returns how many the workgroup has in all.
-__host__ __device__ inline int lin_segments(const PassArgs& A, long long blk, int (*seg)[3],
-                                            int cap) {
-    const long long T = lin_cost(A), nb = A.waves_total, n = A.ra1 - A.ra0;
-    const long long c1 = (blk + 1) * T / nb;
-    long long c = blk * T / nb;
-    int cnt = 0;
-    while (c < c1) {
-        int strip, w;
-        long long base;
-        lin_strip(A, c, strip, base, w);
-        const long long send = base + w * n;  // cost offset past the strip
-        const long long j0 = (c - base + w - 1) / w;
-        long long j1 = ((c1 < send ? c1 : send) - base + w - 1) / w;
-        if (j1 > n) j1 = n;
-        for (long long j = j0; j < j1; j += A.lin_maxr) {
-            if (cnt < cap) {
-                seg[cnt][0] = strip;
-                seg[cnt][1] = (int)(A.ra0 + j);
-                seg[cnt][2] = (int)(A.ra0 + (j1 < j + A.lin_maxr ? j1 : j + A.lin_maxr));
-            }
-            ++cnt;
-        }
-        c = send;
-    }
-    return cnt;
-}
 
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
 hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);

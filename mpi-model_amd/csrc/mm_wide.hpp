@@ -743,8 +743,7 @@ __device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, int iend,
 }
 
 // One strip segment [rA, rB) (local rows) of strip `strip`: this wave's part of it (level
-// group p), carrying the level sums (RED). Every wave of the workgroup passes the same
-// barriers and ends with one, so the LDS ring is free for the next segment.
+// group p), adding the level sums to carry (RED).
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT>
 __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p, int lane,
                                              int strip, int rA, int rB,
@@ -821,90 +820,43 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
         wave_dispatch<C, NA, KW, P, U, B, RED, NT, kBodyEdge>(x, iend, carry);
 }
 
-// The linear plan (A.lin = 1): ONE round of workgroups, waves_total of them (the chip's
-// resident slots), each taking an equal share of the pass. The range's strips are laid
-// end to end in strip order, every row of an interior strip costing 2 units and of the two
-// edge strips (their slower edge body) A.lin_e2 units; workgroup b takes the rows whose
-// cost offset lies in [b*T/n, (b+1)*T/n) -- the tail of one strip and the head of the next,
-// or a run inside one -- as consecutive segments of at most A.lin_maxr rows (buffer
-// offsets below 2^31). Against one workgroup per fixed-length segment this drops the
-// partly filled last round of workgroups and most segment starts (each pays the pipeline
-// fill, (P-1)*D + S0 iterations): a thin slab's 936 segments of 683 rows on 512 slots took
-// two rounds of 735 iterations for 1204 rows of work per slot (mm_internal.hpp
-// lin_segments: the plan's arithmetic, shared with the engine).
-//
 // K = KW * P fused steps per launch of an NA-attribute one-pass program (NA = 1: one
 // diffusion; NA > 1: pre-chain, diffusions of the attributes in diffuse_mask, post-chain),
-// C columns per lane, MW waves per SIMD, P waves per workgroup. Work: the linear plan
-// (A.lin), or one workgroup per strip segment by mm_passk.hpp's seg_map with blocks in
-// place of waves -- the two edge strips first (A.th_edge rows), then the others (A.th
-// rows). RED: every level's sums of the workgroup's output cells into
-// partials[partial_base + block][K][NA]. NT & 1: non-temporal stores.
+// C columns per lane, MW waves per SIMD, P waves per workgroup, one workgroup per strip
+// segment by mm_passk.hpp's seg_map with blocks in place of waves -- the two edge strips
+// first (A.th_edge rows), then the others (A.th rows). RED: every level's sums of the
+// workgroup's output cells into partials[partial_base + block][K][NA]. NT & 1:
+// non-temporal stores.
 template <int C, int NA, int KW, int P, int MW, int U, int B, bool RED, int NT>
 __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     constexpr int RW = 32 * C * NA;  // dv2 per LDS row
     __shared__ dv2 lds[(P > 1 ? P - 1 : 1) * G::RL * RW];
+    const int lane = threadIdx.x & 63;
     const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // level group
     const long long blk = blockIdx.x;
     if (blk >= A.waves_total) return;  // the whole block: no barrier is left waiting
+    int rlo, rhi;
+    long long w = blk;
+    if (w < A.waves_a) {
+        rlo = A.ra0;
+        rhi = A.ra1;
+    } else {
+        w -= A.waves_a;
+        rlo = A.rb0;
+        rhi = A.rb1;
+    }
+    int strip, rA, rB;
+    seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, strip, rA, rB);
     double carry[KW][NA];
 #pragma unroll
     for (int q = 0; q < KW; ++q) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) carry[q][a] = 0.0;
     }
-    // The workgroup's segments (strip, first row, end row) go through LDS: only the
-    // segment counter stays live across the segment loop (the plan's 64-bit arithmetic
-    // held through the hot loop cost it registers: 2x slower, round 5).
-    __shared__ int segs[kLinSegs][3];
-    __shared__ int nsegs;
-    if (threadIdx.x == 0) {
-        int ns = 0;
-        if (A.lin) {
-            ns = lin_segments(A, blk, segs, kLinSegs);
-            ns = ns < kLinSegs ? ns : kLinSegs;  // the engine plans at most kLinSegs
-        } else {
-            int rlo, rhi;
-            long long w = blk;
-            if (w < A.waves_a) {
-                rlo = A.ra0;
-                rhi = A.ra1;
-            } else {
-                w -= A.waves_a;
-                rlo = A.rb0;
-                rhi = A.rb1;
-            }
-            seg_map(w, rlo, rhi, A.nstrips, A.th, A.th_edge, segs[0][0], segs[0][1], segs[0][2]);
-            ns = 1;
-        }
-        nsegs = ns;
-    }
-    __syncthreads();
-    const int nseg = __builtin_amdgcn_readfirstlane(nsegs);
-    for (int si = 0; si < nseg; ++si) {
-        const int strip = __builtin_amdgcn_readfirstlane(segs[si][0]);
-        const int rA = __builtin_amdgcn_readfirstlane(segs[si][1]);
-        const int rB = __builtin_amdgcn_readfirstlane(segs[si][2]);
-        // The kernel arguments are re-read per segment (an opaque zero offset into the
-        // kernarg segment) and the lane index recomputed: hoisted out of this loop, their
-        // values were held through the steady loops, which then reloaded an LDS address
-        // from scratch every row (tools/asm_steady.py; a vmcnt(0) wait per row)
-        int zero = 0;
-        asm volatile("" : "+s"(zero));
-        typedef const __attribute__((address_space(4))) PassArgs KArgs;
-        KArgs* ka = (KArgs*)((const __attribute__((address_space(4))) char*)
-                                 __builtin_amdgcn_kernarg_segment_ptr() + zero);
-        int ln;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-        // (four attributes: A itself -- the chains' scalar operands must stay provably
-        // uniform for chain_asm's SGPR constraints)
-        const PassArgs& As = NA == 1 ? *(const PassArgs*)ka : A;
-        wide_segment<C, NA, KW, P, U, B, RED, NT>(As, lds, p, ln, strip, rA, rB, carry);
-    }
-    if (RED && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
-        // partials[partial_base + block][K][NA]: this wave's KW levels (lane 0)
+    wide_segment<C, NA, KW, P, U, B, RED, NT>(A, lds, p, lane, strip, rA, rB, carry);
+    if (RED && lane == 0) {  // partials[partial_base + block][K][NA]: this wave's KW levels
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
 #pragma unroll

@@ -76,13 +76,6 @@ def test_deep_halo_chain_bit_exact(gpu, O, monkeypatch, H, W, G, k, wide):
     check_deep_chain(gpu, O, monkeypatch, H, W, G, k, wide)
 
 
-@pytest.mark.parametrize("k", WIDE_K)
-@pytest.mark.parametrize("H,W,G", [(100, 488, 3), (300, 700, 2), (64, 300, 2), (41, 200, 8)])
-def test_deep_halo_chain_linear_plan(gpu, O, monkeypatch, H, W, G, k):
-    # the interior of a split pass (and a whole thin slab) on the linear plan
-    check_deep_chain(gpu, O, monkeypatch, H, W, G, k, 1, {"MM_LIN": 1, "MM_LIN_WORKERS": 11})
-
-
 def check_deep_chain(gpu, O, monkeypatch, H, W, G, k, wide, extra=None):
     # wide = 1: the level-split kernel wherever the depth is one of its K (a thinner
     # slab caps the depth to min h, which may leave mm_passk_kernel to run it)
@@ -105,9 +98,7 @@ def check_deep_chain(gpu, O, monkeypatch, H, W, G, k, wide, extra=None):
 
 
 @pytest.mark.parametrize("env", [{}, {"MM_WIDE": 0}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8},
-                                 {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12},
-                                 {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_LIN": 1,
-                                  "MM_LIN_WORKERS": 9}],
+                                 {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12}],
                          ids=lambda e: ",".join(f"{k[3:]}={v}" for k, v in e.items()) or "default")
 @pytest.mark.parametrize("reduce_every", [1, 3])
 @pytest.mark.parametrize("H,W,G", [(100, 488, 3), (41, 200, 8), (300, 700, 2), (130, 257, 4)])

@@ -200,14 +200,7 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1},
-    # the linear plan (one round of workgroups sharing the pass; auto on large slabs),
-    # forced on these small grids: workgroups spanning strips, segments cut at MM_LIN_MAXR
-    # rows, more workgroups than rows (some run nothing), edge rows at the interior cost
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_LIN": 1},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_LIN": 1, "MM_LIN_WORKERS": 7},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_LIN": 1, "MM_LIN_WORKERS": 3, "MM_LIN_MAXR": 17},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_LIN": 1, "MM_LIN_WORKERS": 600, "MM_SEG_EDGE": 1.0},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4, "MM_LIN": 1, "MM_LIN_WORKERS": 2, "MM_KERNEL_VARIANT": 1}]
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4, "MM_KERNEL_VARIANT": 1}]
 
 
 def env_id(env):
@@ -248,9 +241,7 @@ def test_fused_steps_equal_single_steps(gpu, O, monkeypatch, env, shape):
 @pytest.mark.parametrize("env", [{}, {"MM_WIDE": 0}]
                          + [{"MM_WIDE": 0, "MM_STEPS_PER_PASS": k} for k in (3, 2, 8, 6, 7, 10)]
                          + [{"MM_PASSK": 0}]
-                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)]
-                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k, "MM_LIN": 1, "MM_LIN_WORKERS": w,
-                             "MM_LIN_MAXR": 40} for k, w in ((20, 5), (8, 64))],
+                         + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in (4, 8, 12, 16, 20)],
                          ids=env_id)
 @pytest.mark.parametrize("reduce_every", [1, 2, 3, 4, 5])
 def test_fused_steps_step_sums(gpu, O, monkeypatch, env, reduce_every):
