@@ -137,6 +137,8 @@ final() {
     prof c4_k20 c4 1000 50
     prof c2_k8 c2 1000 50
     prof c5_k8 c5 1000 50
+    sq c3_k20 c3 20 5
+    sq c2 c2 1000 50
 }
 
 ab() {  # TAG WL STEPS REPS ENVA ENVB [args]
