@@ -142,8 +142,10 @@ __device__ __forceinline__ double c8_of(int cnt) {
 // grid's first (or last) column as a lane's column 0 (C-1), the columns past it in whole
 // lanes: the lane holding it scales that column by 8/5 (a multiply every lane issues, a
 // select) -- no branch; the columns past the grid keep w = u, and wemit keeps them from
-// crossing into the grid. GEN: any row and strip (the row class is wave-uniform): every
-// column by its own count, 0 outside the grid.
+// crossing into the grid. GEN: any row (the row class sx is wave-uniform): the interior
+// columns' factor and the first / last column's depend on the row only (scalar selects,
+// then EDGE's arithmetic); in a strip the EDGE body cannot run (c.gen) every column by its
+// own count, 0 outside the grid.
 template <int C, int BODY>
 __device__ __forceinline__ void procc(const WLane<C>& c, long long gx, const double (&u)[C],
                                       double (&w)[C]) {
@@ -156,8 +158,18 @@ __device__ __forceinline__ void procc(const WLane<C>& c, long long gx, const dou
         w[C - 1] = c.eR ? w1 : w[C - 1];
     } else if (BODY == kBodyGen) {
         const int sx = span3k(c.H, gx);
+        if (c.gen) {
 #pragma unroll
-        for (int k = 0; k < C; ++k) w[k] = u[k] * c8_of(sx * c.sy[k] - 1);
+            for (int k = 0; k < C; ++k) w[k] = u[k] * c8_of(sx * c.sy[k] - 1);
+        } else {
+            // 3 * sx - 1 neighbours in an interior column, 2 * sx - 1 in the first / last
+            const double fr = c8_of(3 * sx - 1), fe = c8_of(2 * sx - 1);
+            const double w0 = u[0] * fe, w1 = u[C - 1] * fe;
+#pragma unroll
+            for (int k = 0; k < C; ++k) w[k] = u[k] * fr;
+            w[0] = c.eL ? w0 : w[0];
+            w[C - 1] = c.eR ? w1 : w[C - 1];
+        }
     }
 }
 
@@ -205,7 +217,7 @@ __device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx
     for (int k = 0; k < C; ++k) {
         const double cl = k == 0 ? left : cw[k - 1];
         const double cr = k == C - 1 ? right : cw[k + 1];
-        const double m8 = (BODY == kBodyGen && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
+        const double m8 = (BODY == kBodyGen && c.gen && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
         const double t = __builtin_fma(win.um[k], m8, (cl + cr) + pw[k]);
         o[k] = __builtin_fma(t, r8, win.um[k]);
     }
