@@ -46,6 +46,12 @@
 
 #include "mm_passk.hpp"
 
+#ifndef MM_WIDE_GEN_ROW
+// GEN body outside the EDGE-impossible strips: row-uniform weight factors (1) or every
+// column by its own count (0: fewer registers, which the four-attribute instances need)
+#define MM_WIDE_GEN_ROW 1
+#endif
+
 namespace mm {
 
 // per-K entry points (mm_wide_k*.hip: one attribute, C = 4)
@@ -158,7 +164,7 @@ __device__ __forceinline__ void procc(const WLane<C>& c, long long gx, const dou
         w[C - 1] = c.eR ? w1 : w[C - 1];
     } else if (BODY == kBodyGen) {
         const int sx = span3k(c.H, gx);
-        if (c.gen) {
+        if (!MM_WIDE_GEN_ROW || c.gen) {
 #pragma unroll
             for (int k = 0; k < C; ++k) w[k] = u[k] * c8_of(sx * c.sy[k] - 1);
         } else {
@@ -217,7 +223,7 @@ __device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx
     for (int k = 0; k < C; ++k) {
         const double cl = k == 0 ? left : cw[k - 1];
         const double cr = k == C - 1 ? right : cw[k + 1];
-        const double m8 = (BODY == kBodyGen && c.gen && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
+        const double m8 = (BODY == kBodyGen && (!MM_WIDE_GEN_ROW || c.gen) && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
         const double t = __builtin_fma(win.um[k], m8, (cl + cr) + pw[k]);
         o[k] = __builtin_fma(t, r8, win.um[k]);
     }

@@ -18,6 +18,7 @@
 #define MM_WIDE_U 1
 #define MM_WIDE_B 2
 #define MM_CHAIN_ASM 1
+#define MM_WIDE_GEN_ROW 0  // per-column GEN weights: the row-factor body spills here (n4 p1: 125 -> 379)
 #include "mm_wide.hpp"
 
 #define MM_CAT3(a, b, c) a##b##c

@@ -16,6 +16,9 @@
 #define MM_WIDEAR_KW 2
 #endif
 #define MM_CHAIN_RING 1
+// per-column GEN weights: the row-factor GEN body takes this instance from 239 VGPRs and no
+// scratch to 256 + 20 bytes of scratch (the C5 pass 349 -> 374 us on two boxes)
+#define MM_WIDE_GEN_ROW 0
 #define MM_ND 4  // every attribute diffuses (the engine checks)
 #include "mm_wide.hpp"
 
