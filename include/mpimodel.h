@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 4
+#define MM_ABI_VERSION 3
 
 enum mm_status {
     MM_OK = 0,
@@ -107,9 +107,6 @@ typedef struct mm_info {
                                   operands, MM_CHAIN_RUNTIME any chain, its operands
                                   indexed at run time in the register file (chain_asm);
                                   the value 1 is not used */
-    long long linked_launches; /* launches enqueued (or captured) that ran several K-step
-                                  passes linked in one kernel (one rank, one attribute;
-                                  MM_LINK_PASSES=0: off) */
 } mm_info;
 
 /* mm_info.chain_kernel */

@@ -139,19 +139,6 @@ struct mm_engine {
     int graph_count = 0;
     std::string graph_note;
 
-    // linked passes (mm_wide_link_kernel): consecutive K-step passes of one rank's whole
-    // slab in one launch (MM_LINK_PASSES=0: one launch per pass)
-    bool link = true;
-    unsigned long long* link_flags = nullptr;  // per-segment completion flags
-    unsigned* link_ctl = nullptr;              // timeouts (mm::LinkArgs)
-    long long link_launches = 0;               // linked launches enqueued (captures included)
-    bool link_used = false;
-    int link_dbg = 0;                          // MM_LINK_DEBUG
-    std::string link_trace_path;               // MM_LINK_TRACE: per-ticket clocks file
-    unsigned long long* link_trace = nullptr;
-    size_t link_trace_bytes = 0, link_trace_used = 0;
-    long long link_trace_items = 0;
-
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<double> ev_bytes;  // algorithmic bytes of each timed launch (pairs of events)
@@ -663,61 +650,6 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     return MM_OK;
 }
 
-// Segments per pass the link flags cover (one flag each).
-constexpr long long kLinkFlags = 1 << 16;
-// Passes one linked launch holds at most (flags hold epoch << 20 | passes done).
-constexpr int kLinkMaxPasses = 4096;
-
-// Can k-step passes without step sums run linked? One rank owning the whole grid (no
-// halo exchange between passes), one attribute, the level-split kernel with a linked
-// instance of that K.
-bool link_ok(const mm_engine* e, int k) {
-    return e->link && e->link_flags && e->d.nranks == 1 && !e->split && !e->comm &&
-           e->na == 1 && use_wide(e, k) && mm::wide_link_has(k);
-}
-
-// n k-step passes (no step sums) in one launch of the linked kernel: the segment plan of
-// one pass (wide_range), one workgroup per resident slot taking (pass, segment) tickets.
-int enqueue_link(mm_engine* e, int k, int n, bool time_it) {
-    mm::PassArgs A;
-    fill_args(e, e->passes[0], A);
-    A.nstrips = (int)nstrips_wide(e, k);
-    wide_range(e, k, false, A, 0, e->d.h);
-    if (A.waves_total > kLinkFlags) return fail(MM_ERR_STATE, "linked pass: too many segments");
-    mm::LinkArgs X;
-    X.flags = e->link_flags;
-    X.ctl = e->link_ctl;
-    X.npasses = n;
-    X.dbg = e->link_dbg;
-    X.trace = nullptr;
-    if (e->link_trace) {  // MM_LINK_TRACE: the records of the last launch enqueued (a
-                          // fixed buffer: captured graphs keep its address)
-        const size_t need = 4 * sizeof(unsigned long long) * (size_t)(A.waves_total * n);
-        if (need <= e->link_trace_bytes) {
-            e->link_trace_used = need;
-            e->link_trace_items = A.waves_total;
-            X.trace = e->link_trace;
-        }
-    }
-    hipEvent_t a = nullptr, b = nullptr;
-    if (time_it) {
-        a = next_event(e);
-        b = next_event(e);
-        if (!a || !b) return fail(MM_ERR_HIP, "hipEventCreate failed");
-        e->ev_bytes.resize(e->ev_used / 2);
-        e->ev_bytes.back() = 16.0 * (double)e->d.h * (double)e->d.W * n;
-        MM_HIP(hipEventRecord(a, e->s_comp));
-    }
-    MM_HIP(hipMemsetAsync(e->link_flags, 0, sizeof(unsigned long long) * 16 * (size_t)A.waves_total,
-                          e->s_comp));
-    MM_HIP(mm::launch_wide_link(k, A, X, e->s_comp));
-    if (time_it) MM_HIP(hipEventRecord(b, e->s_comp));
-    e->link_launches += 1;
-    e->link_used = true;
-    if (n & 1) e->cur ^= 1;
-    return MM_OK;
-}
-
 // k fused steps of the one-pass program in one mm_passk_kernel pass; bit j of `mask`:
 // append the sums after step j+1 of the pass to the history. Same two-stream structure as
 // enqueue_pass, with a k-row halo (every k steps): the interior rows run as segments
@@ -929,30 +861,12 @@ int enqueue_steps(mm_engine* e, long long first, long long n, long long reduce_e
     long long s = first;
     const long long end = first + n;
     auto red = [&](long long step) { return reduce_every > 0 && step % reduce_every == 0; };
-    auto mask_of = [&](long long s0, int k) {
-        int mask = 0;
-        for (int j = 0; j < k; ++j)
-            if (red(s0 + j)) mask |= 1 << j;
-        return mask;
-    };
     if (passk_ok(e)) {
         while (s < end) {
             const int k = next_pass_len(e, end - s);
-            const int mask = mask_of(s, k);
-            if (mask == 0 && link_ok(e, k)) {  // the run of k-step passes without sums
-                int n = 1;
-                long long s2 = s + k;
-                while (s2 < end && n < kLinkMaxPasses && next_pass_len(e, end - s2) == k &&
-                       mask_of(s2, k) == 0) {
-                    ++n;
-                    s2 += k;
-                }
-                if (n > 1) {
-                    MM_TRY(enqueue_link(e, k, n, time_it));
-                    s = s2;
-                    continue;
-                }
-            }
+            int mask = 0;
+            for (int j = 0; j < k; ++j)
+                if (red(s + j)) mask |= 1 << j;
             MM_TRY(enqueue_passk(e, k, mask, time_it));
             s += k;
         }
@@ -1237,8 +1151,6 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     }
     if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
     if (const char* r = std::getenv("MM_CHAIN_RING")) e->ring_ok = std::atoi(r) != 0;
-    if (const char* l = std::getenv("MM_LINK_PASSES")) e->link = std::atoi(l) != 0;
-    if (const char* l = std::getenv("MM_LINK_DEBUG")) e->link_dbg = std::atoi(l);
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
     // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
     e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
@@ -1284,18 +1196,6 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         hipMalloc(&e->hist_n, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemsetAsync(e->hist_n, 0, 2 * sizeof(unsigned long long), e->s_comp) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "history allocation failed"));
-    if (d.nranks == 1 && d.n_attr == 1 &&
-        (hipMalloc(&e->link_flags, sizeof(unsigned long long) * 16 * kLinkFlags) != hipSuccess ||
-         hipMalloc(&e->link_ctl, 8 * sizeof(unsigned)) != hipSuccess ||
-         hipMemsetAsync(e->link_flags, 0, sizeof(unsigned long long) * 16 * kLinkFlags, e->s_comp) != hipSuccess ||
-         hipMemsetAsync(e->link_ctl, 0, 8 * sizeof(unsigned), e->s_comp) != hipSuccess))
-        return cleanup(fail(MM_ERR_NOMEM, "link flag allocation failed"));
-    if (const char* l = std::getenv("MM_LINK_TRACE")) {
-        e->link_trace_path = l;
-        e->link_trace_bytes = (size_t)64 << 20;
-        if (hipMalloc(&e->link_trace, e->link_trace_bytes) != hipSuccess)
-            return cleanup(fail(MM_ERR_NOMEM, "link trace allocation failed"));
-    }
     e->sum_blocks = std::min<long long>(1024, std::max<long long>(1, d.h));
     if (hipMalloc(&e->sum_tmp, sizeof(double) * (size_t)(e->sum_blocks + mm::kMaxAttr)) != hipSuccess)
         return cleanup(fail(MM_ERR_NOMEM, "sum scratch allocation failed"));
@@ -1369,9 +1269,6 @@ int mm_engine_destroy(mm_engine* e) {
     if (e->hist) (void)hipFree(e->hist);
     if (e->hist_n) (void)hipFree(e->hist_n);
     if (e->sum_tmp) (void)hipFree(e->sum_tmp);
-    if (e->link_flags) (void)hipFree(e->link_flags);
-    if (e->link_ctl) (void)hipFree(e->link_ctl);
-    if (e->link_trace) (void)hipFree(e->link_trace);
     (void)hipGetLastError();  // statuses above are ignored on purpose; do not leave them pending
     delete e;
     return MM_OK;
@@ -1419,7 +1316,6 @@ int mm_engine_info(mm_engine* e, mm_info* info) {
     info->graph_count = e->graph_count;
     info->graph_launches = e->graph_launches;
     info->hist_entries = e->hist_host;
-    info->linked_launches = e->link_launches;
     std::snprintf(info->graph_note, sizeof info->graph_note, "%s", e->graph_note.c_str());
     return MM_OK;
 }
@@ -1446,8 +1342,6 @@ int mm_upload(mm_engine* e, int attr, const double* host) {
     return MM_OK;
 }
 
-int link_check(mm_engine* e);
-
 int mm_download(mm_engine* e, int attr, double* host) {
     if (!e || !host || attr < 0 || attr >= e->na) return fail(MM_ERR_INVALID, "mm_download: bad arguments");
     MM_TRY(set_device(e));
@@ -1456,7 +1350,7 @@ int mm_download(mm_engine* e, int attr, double* host) {
                             sizeof(double) * e->pitch, sizeof(double) * e->d.W, e->d.h,
                             hipMemcpyDeviceToHost, e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comp));
-    return link_check(e);
+    return MM_OK;
 }
 
 int mm_clear_flows(mm_engine* e) {
@@ -1723,38 +1617,12 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
     return finish();
 }
 
-// After the streams drained: a linked launch whose segment waits gave up (kLinkSpins) ran
-// on rows that may not have been written yet -- an error, never a silent result.
-int link_check(mm_engine* e) {
-    if (!e->link_used) return MM_OK;
-    if (e->link_trace && e->link_trace_used) {  // MM_LINK_TRACE: items, then the records
-        std::vector<unsigned long long> h(e->link_trace_used / sizeof(unsigned long long));
-        MM_HIP(hipMemcpy(h.data(), e->link_trace, e->link_trace_used, hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(e->link_trace_path.c_str(), "wb")) {
-            const unsigned long long items = (unsigned long long)e->link_trace_items;
-            std::fwrite(&items, sizeof items, 1, f);
-            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
-            std::fclose(f);
-        }
-    }
-    unsigned c[8] = {};
-    MM_HIP(hipMemcpy(c, e->link_ctl, sizeof c, hipMemcpyDeviceToHost));
-    if (c[3]) {
-        char msg[200];
-        std::snprintf(msg, sizeof msg,
-                      "linked passes: %u segment wait(s) timed out (first: flag %u held %u:%u, "
-                      "needed %u)", c[3], c[4], c[7], c[5], c[6]);
-        return fail(MM_ERR_HIP, msg);
-    }
-    return MM_OK;
-}
-
 int mm_synchronize(mm_engine* e) {
     if (!e) return fail(MM_ERR_INVALID, "mm_synchronize: null");
     MM_TRY(set_device(e));
     MM_HIP(hipStreamSynchronize(e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comm));
-    return link_check(e);
+    return MM_OK;
 }
 
 int mm_sums(mm_engine* e, double* out) {

@@ -47,17 +47,6 @@ struct PassArgs {
     int th_edge;            // mm_passk_kernel segments: rows per wave of the two edge strips
 };
 
-// Linked passes of the wide kernel (mm_wide_link_kernel): per-segment completion flags
-// and the launch's control words, device memory the engine keeps (zeroed once).
-struct LinkArgs {
-    unsigned long long* flags;  // [segments of one pass]: passes done (zeroed per launch)
-    unsigned* ctl;              // [3] timeouts, [4..7] the first timeout: flag index, value
-                                // seen (low, high word at [7]), value needed
-    int npasses;
-    int dbg;  // MM_LINK_DEBUG: bit 2 skips the acquire (measurement only)
-    unsigned long long* trace;  // MM_LINK_TRACE: [ticket][4] clocks + XCD, or null
-};
-
 // Launchers (mm_kernels.hip). All enqueue on `s` and return the launch status.
 hipError_t launch_pass(int na, bool reduce, const PassArgs& a, hipStream_t s, int variant);
 // K fused steps of a one-pass flow program (NA = 1: K 1..10, one diffusion; NA 2..4:
@@ -89,10 +78,6 @@ int wide_waves_per_block(int k, int c, int na, bool ring);
 int wide_blocks_per_cu(int k, int c, int na, bool red, int nt);
 hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
                        int variant);
-// npasses linked K-step passes of one attribute in one launch (K with wide_link_has);
-// a: the first pass's arguments, one row range.
-bool wide_link_has(int k);
-hipError_t launch_wide_link(int k, const PassArgs& a, const LinkArgs& x, hipStream_t s);
 // Append the levels of `mask` (bit j: step j of a K-step pass) of partials[n][k][na],
 // each summed in a fixed order, to the history (na sums per entry).
 // perm: partials slot i holds attribute (perm >> 2i) & 3 (relabelled passes).

@@ -190,12 +190,4 @@ hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStr
     }
 }
 
-bool wide_link_has(int k) { return k == 8; }
-
-hipError_t launch_wide_link(int k, const PassArgs& a, const LinkArgs& x, hipStream_t s) {
-    if (a.waves_total <= 0) return hipSuccess;
-    if (k == 8) return wide_link_launch_k8(a, x, s);
-    return hipErrorInvalidValue;
-}
-
 }  // namespace mm

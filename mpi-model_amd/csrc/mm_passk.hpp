@@ -186,10 +186,8 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, unsigned off
     dv2 v;
     v.x = w0;
     v.y = w1;
-    // NT bit 0: non-temporal; bit 1: write-through (sc1), for rows another workgroup of
-    // the same launch reads after a flag (mm_wide_link_kernel)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0,
-                                           (NT & 1) ? 2 : ((NT & 2) ? 16 : 0));
+                                           (NT & 1) ? 2 : 0);
 }
 
 // One level's three-row window of one attribute: the weights of the row above (wa) and of

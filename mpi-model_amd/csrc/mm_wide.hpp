@@ -65,8 +65,6 @@ MM_WIDE_DECL(16)
 MM_WIDE_DECL(20)
 #undef MM_WIDE_DECL
 int wide_waves_k20();  // waves per workgroup of the K = 20 instance
-// linked passes (mm_wide_link_kernel) of the K = 8 instance
-hipError_t wide_link_launch_k8(const PassArgs& a, const LinkArgs& x, hipStream_t s);
 // four attributes, 2 columns per lane. K = 4 (mm_widea_k4.hip): any pass.
 hipError_t widea_launch_k4(int na, bool red, const PassArgs& a, hipStream_t s, int v);
 int widea_blocks_k4(int na, bool red, int nt);
@@ -763,11 +761,11 @@ __device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, int iend,
 }
 
 // One strip segment [rA, rB) (local rows) of strip `strip`: this wave's part of it (level
-// group p), adding the level sums to carry (RED). par: the buffers' roles (linked passes).
+// group p), adding the level sums to carry (RED).
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT>
 __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p, int lane,
                                              int strip, int rA, int rB,
-                                             double (&carry)[KW][NA], int par = 0) {
+                                             double (&carry)[KW][NA]) {
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     constexpr int LH = (K + C - 1) / C;       // halo lanes per side
@@ -805,11 +803,9 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         x.r8[a] = A.drate[a] * 0.125;
-        // par = 1: the pass reads A.out and writes A.in (the odd passes of a chain)
-        const double* src = par ? A.out[a] : A.in[a];
-        double* dst = par ? const_cast<double*>(A.in[a]) : A.out[a];
-        x.in[a] = rows_rsrc(src + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K, A.pitch);
-        x.out[a] = rows_rsrc(dst + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
+        x.in[a] = rows_rsrc(A.in[a] + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K,
+                            A.pitch);
+        x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
     }
     x.lds_in = p > 0 ? lds + (p - 1) * G::RL * RW : lds;
     x.lds_out = p < P - 1 ? lds + p * G::RL * RW : lds;
@@ -886,191 +882,6 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
                 A.partials[((A.partial_base + blk) * K + p * KW + q) * NA + a] = carry[q][a];
         }
     }
-}
-
-// Linked passes: X.npasses K-step passes of one attribute over one rank's whole slab (one
-// row range, no halo) in ONE launch of one workgroup per (pass, segment): workgroup b runs
-// ticket b -- pass-major, each pass's segments in seg_map order -- so one pass's segments
-// start while the previous pass's last ones still run, and no kernel boundary separates
-// the passes. Pass q reads the buffer pass q-1 wrote (ping-pong: even passes A.in ->
-// A.out, odd passes back), so a segment of pass q waits for the pass q-1 segments whose
-// rows it reads: strips s-1..s+1, rows [rA - K, rB + K). Those are also every segment of
-// pass q-1 that reads the rows it overwrites (the neighbourhoods are symmetric), so no
-// other ordering is needed. A workgroup waits only on lower tickets; the dispatcher starts
-// each XCD's workgroups in index order, so the lowest unfinished ticket is running and
-// never waits. (A global ticket counter instead of the index makes that order explicit
-// but costs two device-scope atomics per workgroup: C2 1389 vs 1660 GCUPS unlinked.)
-//
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the segment's rows are
-// stored write-through (sc1), the storing wave drains them (vmcnt 0), a workgroup barrier,
-// then one lane stores the segment's flag (agent scope). The consumer's wave 0 polls its
-// producers' flags (one per lane, agent-scope loads), then an agent acquire and a barrier
-// before any wave loads. The engine zeroes the flags before each launch (flag = passes
-// done). A poll gives up after kLinkSpins tries and counts a timeout (X.ctl[3]; the engine
-// turns it into an error at the next synchronisation) instead of hanging the GPU.
-constexpr unsigned kLinkSpins = 1u << 16;
-// one flag per 128-B line (pollers of different flags meet in no L2 channel line); the
-// flags a segment waits on are polled by kLinkLanes lanes, s_sleep MM_LINK_SLEEP between
-// polls (every waiting workgroup polls beside the running ones' HBM streams)
-constexpr int kLinkPad = 16;
-#ifndef MM_LINK_LANES
-#define MM_LINK_LANES 1
-#endif
-constexpr int kLinkLanes = MM_LINK_LANES;
-#ifndef MM_LINK_SLEEP
-#define MM_LINK_SLEEP 8
-#endif
-
-// item index of row block rb of strip `strip` (the inverse of seg_map)
-__device__ __forceinline__ long long seg_item(int strip, int rb, int n, int ns, int r, int re) {
-    if (ns < 3) return (long long)rb * ns + strip;
-    const int nbe = (n + re - 1) / re;
-    if (strip == 0) return rb;
-    if (strip == ns - 1) return nbe + rb;
-    const int nb = (n + r - 1) / r;
-    const int q = rb == 0 ? 0 : (rb == nb - 1 ? 1 : rb + 1);
-    return 2LL * nbe + (long long)q * (ns - 2) + (strip - 1);
-}
-
-// The linked launch's order of one pass's segments: by rows, so that a pass's first
-// segments read rows the previous pass finished first. Group q holds the interior strips'
-// row block q (strips 1..ns-2), then the edge strips' segments starting in its rows (strip
-// 0's, then strip ns-1's; E(q) = ceil(min(q r, n) / re) edge segments start before it).
-// Returns the seg_map index of in-pass ticket t (the flags are indexed by it) and the
-// segment. Narrow grids (ns < 3) keep seg_map's order, already by rows.
-__device__ __forceinline__ unsigned link_map(unsigned t, int lo, int hi, int ns, int r, int re,
-                                             int& strip, int& rA, int& rB) {
-    const int n = hi - lo;
-    if (ns < 3) {
-        seg_map(t, lo, hi, ns, r, re, strip, rA, rB);
-        return t;
-    }
-    const int nb = (n + r - 1) / r;
-    auto E = [&](int q) { return (min(q * r, n) + re - 1) / re; };
-    auto start = [&](int q) { return (unsigned)(q * (ns - 2) + 2 * E(q)); };
-    int qa = 0, qb = nb - 1;  // the last q with start(q) <= t
-    while (qa < qb) {
-        const int m = (qa + qb + 1) / 2;
-        if (start(m) <= t) qa = m; else qb = m - 1;
-    }
-    const int q = qa;
-    const int o = (int)(t - start(q));
-    int rb, rows;
-    if (o < ns - 2) {
-        strip = 1 + o;
-        rb = q;
-        rows = r;
-    } else {
-        const int o2 = o - (ns - 2), cnt = E(q + 1) - E(q);
-        strip = o2 < cnt ? 0 : ns - 1;
-        rb = E(q) + (o2 < cnt ? o2 : o2 - cnt);
-        rows = re;
-    }
-    rA = lo + rb * rows;
-    rB = min(rA + rows, hi);
-    return (unsigned)seg_item(strip, rb, n, ns, r, re);
-}
-
-// wave 0: wait until every pass-(pass-1) segment under strips strip-1..strip+1, rows
-// [rA - K, rB + K) has stored its rows, then acquire them for this CU
-template <int K>
-__device__ __forceinline__ void link_wait(const PassArgs& A, const LinkArgs& X, int lane,
-                                          int strip, int rA, int rB, unsigned long long need,
-                                          bool acquire) {
-    const int lo = A.ra0, hi = A.ra1, n = hi - lo, ns = A.nstrips;
-    const int s0 = strip > 0 ? strip - 1 : 0, s1 = strip < ns - 1 ? strip + 1 : ns - 1;
-    const int r0 = max(lo, rA - K), r1 = min(hi, rB + K);  // rows read, [r0, r1)
-    unsigned spins = 0;
-    int j = 0;  // dependency index; lane l takes l, l + 64, ...
-    for (int sd = s0; sd <= s1; ++sd) {
-        const int rows = (ns < 3 || sd == 0 || sd == ns - 1) ? A.th_edge : A.th;
-        const int b0 = (r0 - lo) / rows, b1 = (r1 - 1 - lo) / rows;
-        for (int rb = b0; rb <= b1; ++rb, ++j) {
-            if (j % kLinkLanes != lane) continue;
-            const unsigned long long* f = X.flags + kLinkPad * seg_item(sd, rb, n, ns, A.th, A.th_edge);
-            unsigned long long v;
-            while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
-                if (++spins > kLinkSpins) {
-                    // the first timeout of a launch records what it saw (mm_engine.hip)
-                    if (__hip_atomic_fetch_add(X.ctl + 3, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                        X.ctl[4] = (unsigned)((f - X.flags) / kLinkPad);
-                        X.ctl[5] = (unsigned)v;
-                        X.ctl[6] = (unsigned)need;
-                        X.ctl[7] = (unsigned)(v >> 32);
-                    }
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(MM_LINK_SLEEP);
-            }
-        }
-    }
-    if (acquire) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-template <int C, int KW, int P, int MW, int U, int B, int NT>
-__global__ __launch_bounds__(64 * P, MW) void mm_wide_link_kernel(const PassArgs A,
-                                                                  const LinkArgs X) {
-    using G = WGeom<KW, P, B>;
-    constexpr int K = G::K;
-    constexpr int RW = 32 * C;  // dv2 per LDS row
-    __shared__ dv2 lds[(P > 1 ? P - 1 : 1) * G::RL * RW];
-    const int lane = threadIdx.x & 63;
-    const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const unsigned items = (unsigned)A.waves_total;
-    const unsigned t = blockIdx.x;  // the ticket
-    const unsigned pass = t / items;
-    int strip, rA, rB;
-    const unsigned item = (X.dbg & 8) ? t - pass * items
-                                      : link_map(t - pass * items, A.ra0, A.ra1, A.nstrips,
-                                                 A.th, A.th_edge, strip, rA, rB);
-    if (X.dbg & 8) seg_map(item, A.ra0, A.ra1, A.nstrips, A.th, A.th_edge, strip, rA, rB);
-    unsigned long long t0 = 0, t1 = 0;
-    if (X.trace && threadIdx.x == 0) t0 = wall_clock64();
-    if (pass > 0 && p == 0) link_wait<K>(A, X, lane, strip, rA, rB, pass, !(X.dbg & 4));
-    if (X.trace && threadIdx.x == 0) t1 = wall_clock64();
-    __syncthreads();
-    double carry[KW][1];
-    wide_segment<C, 1, KW, P, U, B, false, NT>(A, lds, p, lane, strip, rA, rB, carry,
-                                              (int)(pass & 1));
-    if (p == P - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its rows stored
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (!(NT & 2)) {  // plain stores: write the XCD's L2 back before the flag
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __hip_atomic_store(X.flags + kLinkPad * item, (unsigned long long)pass + 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        if (X.trace) {  // MM_LINK_TRACE: start, waited, done (wall clock) and the XCD
-            unsigned long long* r = X.trace + 4 * (unsigned long long)t;
-            r[0] = t0;
-            r[1] = t1;
-            r[2] = wall_clock64();
-            r[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-        }
-    }
-}
-
-// One launch of X.npasses linked passes (a.seg set, one row range): one workgroup per
-// (pass, segment).
-template <int C, int KW, int P, int MW>
-hipError_t wide_link_launch2(const PassArgs& a, const LinkArgs& x, hipStream_t s) {
-    const long long n = a.waves_total * (long long)x.npasses;
-    if (!a.seg || a.rb1 > a.rb0 || x.npasses < 1 || n < 1 || n >= (1LL << 31))
-        return hipErrorInvalidValue;
-    (void)hipGetLastError();
-    // MM_LINK_DEBUG bit 5: plain stores + an agent release before the flag
-    if (x.dbg & 32)
-        hipLaunchKernelGGL((mm_wide_link_kernel<C, KW, P, MW, MM_WIDE_U, MM_WIDE_B, 0>),
-                           dim3((unsigned)n), dim3(64 * P), 0, s, a, x);
-    else
-        hipLaunchKernelGGL((mm_wide_link_kernel<C, KW, P, MW, MM_WIDE_U, MM_WIDE_B, 2>),
-                           dim3((unsigned)n), dim3(64 * P), 0, s, a, x);
-    return hipGetLastError();
 }
 
 template <int C, int NA, int KW, int P, int MW, int NT>

@@ -27,9 +27,5 @@ hipError_t wide_launch_k8(bool red, const PassArgs& a, hipStream_t s, int v) {
 
 int wide_blocks_k8(bool red, int nt) { return wide_blocks<4, 1, 2, 4, MM_WIDE_MIN_WAVES>(red, nt); }
 
-hipError_t wide_link_launch_k8(const PassArgs& a, const LinkArgs& x, hipStream_t s) {
-    return wide_link_launch2<4, 2, 4, MM_WIDE_MIN_WAVES>(a, x, s);
-}
-
 
 }  // namespace mm

@@ -68,7 +68,7 @@ class Info(ctypes.Structure):
                 ("graph_state", ctypes.c_int), ("graph_count", ctypes.c_int),
                 ("graph_launches", ctypes.c_longlong), ("hist_entries", ctypes.c_longlong),
                 ("graph_note", ctypes.c_char * 160), ("seg_waves_per_cu", ctypes.c_int),
-                ("chain_kernel", ctypes.c_int), ("linked_launches", ctypes.c_longlong)]
+                ("chain_kernel", ctypes.c_int)]
 
 
 _lib = None

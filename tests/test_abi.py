@@ -47,7 +47,7 @@ def test_library_exports_every_declared_symbol(mm):
     L = mm.lib()
     for name in declared_functions():
         assert hasattr(L, name), name
-    assert L.mm_abi_version() == 4
+    assert L.mm_abi_version() == 3
 
 
 def test_step_count(mm, O):
