@@ -573,7 +573,11 @@ void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lo
     if (!bpc) bpc = std::max(1, mm::wide_blocks_per_cu(k, c, e->na, red, nt));
     const long long n = hi - lo, ns = A.nstrips;
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
-    const double edge = e->seg_edge > 0.0 ? e->seg_edge : 0.5;
+    // edge strips: full-length segments for one attribute (the EDGE / GEN bodies cost
+    // little more than the interior's since round 5: c2 / c3 +0.5-1.5 %, c4 and the split
+    // slabs within +-1 %), half length for four (their per-column GEN body: C5 -10 % at
+    // full length; profiles/r05/edge)
+    const double edge = e->seg_edge > 0.0 ? e->seg_edge : (e->na == 1 ? 1.0 : 0.5);
     const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
     auto re_of = [&](long long rr) {
         return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
