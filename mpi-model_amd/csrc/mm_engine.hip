@@ -562,8 +562,8 @@ long long nstrips_wide(const mm_engine* e, int k) {
 
 // Segment plan of rows [lo, hi) for the wide kernel: one workgroup per strip segment, r
 // rows per interior-strip segment and re per edge-strip segment, the smallest r for which
-// the blocks fit seg_waves x the chip's resident blocks. Auto: 4 per resident slot, halved
-// (down to 1) while segments are shorter than 24 K rows -- a segment pays 3K - 1 pipeline
+// the blocks fit seg_waves x the chip's resident blocks. Auto: 4 per resident slot, fewer
+// (down to 1) while segments are shorter than 20 K rows -- a segment pays 3K - 1 pipeline
 // iterations and 2K extra input rows, 15 % of a 318-row segment at K = 16 (4096 x 32768,
 // profiles/r03/kernel_table).
 void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, long long hi) {
@@ -593,10 +593,14 @@ void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lo
     if (e->seg_waves > 0.0) {
         r = plan(e->seg_waves);
     } else {
+        // 4, 3, 2, 1 segment waves per slot while segments are shorter than 20 K rows: the
+        // 4096 x 32768 split slab of an 8-GPU c3 run takes 3 (460-row segments; 2 gave 683:
+        // kernel 1000-1022 vs 1069-1082 us, 200 steps +2.9 %, profiles/r05/sw3); the other
+        // bench shapes keep their plans (c2 ends at 1, 32768^2 / 16384^2 / 8192-row slabs at 4)
         double sw = 4.0;
         r = plan(sw);
-        while (sw > 1.0 && r < 24LL * k) {
-            sw *= 0.5;
+        while (sw > 1.0 && r < 20LL * k) {
+            sw -= 1.0;
             r = plan(sw);
         }
     }
