@@ -62,7 +62,8 @@ static void exchange(slab* s, double* vg) {
 /* one diffusion of attribute a (the vn buffer becomes the attribute's buffer) */
 static void diffuse(slab* s, int a, double rate) {
     exchange(s, s->vg[a]);
-    or_field_step_slab(s->H, s->W, s->x0, s->h, s->vg[a], s->vn + s->W, rate);
+    if (or_field_step_slab(s->H, s->W, s->x0, s->h, s->vg[a], s->vn + s->W, rate) != 0)
+        MPI_Abort(MPI_COMM_WORLD, 3);  /* out of memory */
     double* t = s->vg[a];
     s->vg[a] = s->vn;
     s->vn = t;

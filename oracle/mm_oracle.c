@@ -117,9 +117,11 @@ static void w_row(long long H, long long W, long long gx, const double* vrow, do
 /* rows(gx) gives the v row for any global gx in [x_lo-1, x_hi]. */
 typedef const double* (*row_fn)(const void* ctx, long long gx);
 
-static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
-                      row_fn rows, const void* ctx, double* vout, double rate) {
+/* returns 0, or -1 when its row buffers cannot be allocated (nothing written) */
+static int step_rows(long long H, long long W, long long x_lo, long long x_hi,
+                     row_fn rows, const void* ctx, double* vout, double rate) {
     double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
+    if (!buf) return -1;
     double* w_prev = buf;
     double* w_cur = buf + W;
     double* w_next = buf + 2 * W;
@@ -150,6 +152,7 @@ static void step_rows(long long H, long long W, long long x_lo, long long x_hi,
         w_next = t;
     }
     free(buf);
+    return 0;
 }
 
 typedef struct {
@@ -164,15 +167,15 @@ static const double* grid_row(const void* ctx_, long long gx) {
     return c->v + (gx - c->base) * c->W;
 }
 
-void or_field_step(long long H, long long W, const double* v, double* vout, double rate) {
+int or_field_step(long long H, long long W, const double* v, double* vout, double rate) {
     grid_ctx c = {v, H, W, 0, 0, H};
-    step_rows(H, W, 0, H, grid_row, &c, vout, rate);
+    return step_rows(H, W, 0, H, grid_row, &c, vout, rate);
 }
 
-void or_field_step_slab(long long H, long long W, long long x_init, long long h,
-                        const double* vg, double* vout, double rate) {
+int or_field_step_slab(long long H, long long W, long long x_init, long long h,
+                       const double* vg, double* vout, double rate) {
     grid_ctx c = {vg, H, W, x_init - 1, x_init - 1, x_init + h + 1};
-    step_rows(H, W, x_init, x_init + h, grid_row, &c, vout, rate);
+    return step_rows(H, W, x_init, x_init + h, grid_row, &c, vout, rate);
 }
 
 /* step_rows with the counts hoisted: rows strictly inside the grid have cnt == 8 except in
@@ -193,11 +196,11 @@ static OR_FAST_TARGET void w_row_fast(long long H, long long W, long long gx,
     w[W - 1] = vrow[W - 1] * c8_of(or_neighbor_count(H, W, gx, W - 1));
 }
 
-static OR_FAST_TARGET void step_rows_fast(long long H, long long W, long long x_lo,
-                                          long long x_hi, row_fn rows, const void* ctx,
-                                          double* vout, double rate) {
+static OR_FAST_TARGET int step_rows_fast(long long H, long long W, long long x_lo,
+                                         long long x_hi, row_fn rows, const void* ctx,
+                                         double* vout, double rate) {
     double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
-    if (!buf) return;
+    if (!buf) return -1;
     double* w_prev = buf;
     double* w_cur = buf + W;
     double* w_next = buf + 2 * W;
@@ -233,6 +236,7 @@ static OR_FAST_TARGET void step_rows_fast(long long H, long long W, long long x_
         w_next = t;
     }
     free(buf);
+    return 0;
 }
 
 static int fast_ok(void) {
@@ -266,10 +270,13 @@ int or_field_rows(long long H, long long W, long long lo, long long hi, int step
         const long long elo = lo - steps + st > 0 ? lo - steps + st : 0;
         const long long ehi = hi + steps - st < H ? hi + steps - st : H;
         grid_ctx c = {a, H, W, clo, plo, phi};
-        if (fast)
-            step_rows_fast(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate);
-        else
-            step_rows(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate);
+        const int rc = fast ? step_rows_fast(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate)
+                            : step_rows(H, W, elo, ehi, grid_row, &c, b + (elo - clo) * W, rate);
+        if (rc != 0) {  /* out of memory: the caller raises, never compares garbage */
+            free(a);
+            free(b);
+            return -1;
+        }
         double* t = a;
         a = b;
         b = t;
@@ -282,9 +289,10 @@ int or_field_rows(long long H, long long W, long long lo, long long hi, int step
     return 0;
 }
 
-void or_field_step_general(long long H, long long W, const double* v, const double* outf,
-                           double* vout) {
-    double* s = (double*)malloc(sizeof(double) * (size_t)(H * W));
+int or_field_step_general(long long H, long long W, const double* v, const double* outf,
+                          double* vout) {
+    double* s = (double*)malloc(sizeof(double) * (size_t)(H * W > 0 ? H * W : 1));
+    if (!s) return -1;
     for (long long x = 0; x < H; ++x)
         for (long long y = 0; y < W; ++y)
             s[x * W + y] = share_of(outf[x * W + y], or_neighbor_count(H, W, x, y));
@@ -299,16 +307,17 @@ void or_field_step_general(long long H, long long W, const double* v, const doub
         }
 #undef S
     free(s);
+    return 0;
 }
 
-void or_program_step(long long H, long long W, int n_attr, double* const* v,
-                     const or_flow* flows, int n_flows, double* scratch) {
+int or_program_step(long long H, long long W, int n_attr, double* const* v,
+                    const or_flow* flows, int n_flows, double* scratch) {
     const long long n = H * W;
     for (int f = 0; f < n_flows; ++f) {
         const or_flow* fl = &flows[f];
         if (fl->a < 0 || fl->a >= n_attr) continue;
         if (fl->kind == 1) {
-            or_field_step(H, W, v[fl->a], scratch, fl->rate);
+            if (or_field_step(H, W, v[fl->a], scratch, fl->rate) != 0) return -1;
             memcpy(v[fl->a], scratch, sizeof(double) * (size_t)n);
         } else if (fl->kind == 2) {
             double* va = v[fl->a];
@@ -320,6 +329,7 @@ void or_program_step(long long H, long long W, int n_attr, double* const* v,
             }
         }
     }
+    return 0;
 }
 
 double or_sum(const double* v, size_t n) {

@@ -71,9 +71,13 @@ def lib():
         L.or_neighbor_count.argtypes = [LL, LL, LL, LL]
         L.or_fill_random.argtypes = [LL, LL, LL, LL, ctypes.c_uint64, P]
         L.or_point_apply.argtypes = [LL, LL, P, LL, LL, D, D]
+        L.or_field_step.restype = I
         L.or_field_step.argtypes = [LL, LL, P, P, D]
+        L.or_field_step_slab.restype = I
         L.or_field_step_slab.argtypes = [LL, LL, LL, LL, P, P, D]
+        L.or_field_step_general.restype = I
         L.or_field_step_general.argtypes = [LL, LL, P, P, P]
+        L.or_program_step.restype = I
         L.or_program_step.argtypes = [LL, LL, I, P, ctypes.POINTER(OrFlow), I, P]
         L.or_field_rows.restype = I
         L.or_field_rows.argtypes = [LL, LL, LL, LL, I, D, ctypes.c_uint64, P]
@@ -81,6 +85,11 @@ def lib():
         L.or_sum.argtypes = [P, ctypes.c_size_t]
         _lib = L
     return _lib
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise MemoryError(f"{what}: out of memory")
 
 
 def _ptr(a):
@@ -131,7 +140,7 @@ def field_step(v, rate, steps=1):
     H, W = v.shape
     o = np.empty_like(v)
     for _ in range(steps):
-        lib().or_field_step(H, W, _ptr(v), _ptr(o), rate)
+        _ok(lib().or_field_step(H, W, _ptr(v), _ptr(o), rate), "or_field_step")
         v, o = o, v
     return v
 
@@ -141,7 +150,7 @@ def field_step_general(v, outf):
     outf = np.ascontiguousarray(outf, dtype=np.float64)
     H, W = v.shape
     o = np.empty_like(v)
-    lib().or_field_step_general(H, W, _ptr(v), _ptr(outf), _ptr(o))
+    _ok(lib().or_field_step_general(H, W, _ptr(v), _ptr(outf), _ptr(o)), "or_field_step_general")
     return o
 
 
@@ -150,7 +159,7 @@ def field_step_slab(H, W, x_init, vg, rate):
     vg = np.ascontiguousarray(vg, dtype=np.float64)
     h = vg.shape[0] - 2
     o = np.empty((h, W), dtype=np.float64)
-    lib().or_field_step_slab(H, W, x_init, h, _ptr(vg), _ptr(o), rate)
+    _ok(lib().or_field_step_slab(H, W, x_init, h, _ptr(vg), _ptr(o), rate), "or_field_step_slab")
     return o
 
 
@@ -191,7 +200,8 @@ def program_step(fields, flows, steps=1, sums_per_step=False):
     scratch = np.empty((H, W), dtype=np.float64)
     sums = []
     for _ in range(steps):
-        lib().or_program_step(H, W, len(fields), arr, fl, len(flows), _ptr(scratch))
+        _ok(lib().or_program_step(H, W, len(fields), arr, fl, len(flows), _ptr(scratch)),
+            "or_program_step")
         if sums_per_step:
             sums.append([float(np.sum(f, dtype=np.float64)) for f in fields])
     return (fields, sums) if sums_per_step else fields

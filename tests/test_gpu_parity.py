@@ -198,7 +198,7 @@ WIDE_ENVS = [{"MM_WIDE": 1}] + [{"MM_WIDE": 1, "MM_STEPS_PER_PASS": k} for k in 
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 8, "MM_SEG_WAVES": 64},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_SEG_WAVES": 0.01},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 16, "MM_SEG_EDGE": 1.0},
-    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_XCD_REMAP": 1},
+    {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 20, "MM_SEG_WAVES": 3},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 12, "MM_KERNEL_VARIANT": 1},
     {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4, "MM_KERNEL_VARIANT": 1}]
 
@@ -392,7 +392,7 @@ WIDE_PROGRAMS = [
 
 @pytest.mark.parametrize("env", [{"MM_WIDE": 1}, {"MM_WIDE": 1, "MM_STEPS_PER_PASS": 4},
                                  {"MM_WIDE": 1, "MM_SEG_WAVES": 0.01},
-                                 {"MM_WIDE": 1, "MM_XCD_REMAP": 1, "MM_KERNEL_VARIANT": 1},
+                                 {"MM_WIDE": 1, "MM_KERNEL_VARIANT": 1},
                                  # variant bits beyond 0 must not select the ring instance
                                  # for a program that is not the ring
                                  {"MM_WIDE": 1, "MM_KERNEL_VARIANT": 3},

@@ -64,6 +64,58 @@ def test_uniform_rate_step_equals_general_form(O, shape):
     assert np.max(np.abs(got - want) / np.abs(want)) <= 1e-14
 
 
+def _emitter_steps(O, v, rate, steps):
+    """The reference's own update iterated: every cell with neighbours emits out = r*v and
+    each neighbour receives out/cnt (or_field_step_general, src/Model.hpp:199,206-211,234;
+    src/Exponencial.hpp:14-16)."""
+    H, W = v.shape
+    emits = np.array([[O.neighbor_count(H, W, x, y) > 0 for y in range(W)] for x in range(H)])
+    for _ in range(steps):
+        v = O.field_step_general(v, np.where(emits, rate * v, 0.0))
+    return v
+
+
+# 2-row, 2-column, 2x2 and 3x3 grids are all edge / corner cells (the rounded 8/5 and 8/3
+# weights of the per-receiver form dominate); 64x96 and 130x97 mix every count class
+@pytest.mark.parametrize("shape,steps", [((2, 50), 1000), ((50, 2), 1000), ((2, 2), 1000),
+                                         ((3, 3), 1000), ((64, 96), 1000), ((130, 97), 1000),
+                                         ((200, 300), 20), ((1, 9), 20)])
+@pytest.mark.parametrize("rate", [0.1, 0.3])
+def test_whole_grid_step_tracks_reference_update_over_bench_steps(O, shape, steps, rate):
+    """The kernels' (and the oracle's) per-receiver step against the reference's
+    per-emitter update, iterated over the bench runs' step counts (20: the driver's line;
+    1000: the long lines). Bound: north_star's 1e-12 relative per cell; measured <= 2.2e-14
+    (DESIGN.md section 2). Both forms conserve the total to the same bound."""
+    v = O.fill_random(*shape)
+    got, want = O.field_step(v, rate, steps=steps), _emitter_steps(O, v, rate, steps)
+    assert np.max(np.abs(got - want) / np.abs(want)) <= 1e-12
+    s0 = math.fsum(v.ravel())
+    for f in (got, want):
+        assert abs(math.fsum(f.ravel()) - s0) <= 1e-12 * s0
+
+
+@pytest.mark.parametrize("shape", [(2, 50), (3, 3), (64, 96)])
+def test_program_diffusions_track_reference_update_over_1000_steps(O, shape):
+    """C5's flow program (transfer ring, then four diffusions) with each diffusion as the
+    reference's per-emitter update, against or_program_step (the kernels' per-receiver
+    form), 1000 steps: every attribute within 1e-12 relative (measured <= 8.2e-15)."""
+    H, W = shape
+    emits = np.array([[O.neighbor_count(H, W, x, y) > 0 for y in range(W)] for x in range(H)])
+    fields = [O.fill_random(H, W, seed=O.SEED + a) for a in range(4)]
+    want = [f.copy() for f in fields]
+    for _ in range(1000):
+        for kind, a, b, r in C5_FLOWS:
+            if kind == O.DIFFUSE:
+                want[a] = O.field_step_general(want[a], np.where(emits, r * want[a], 0.0))
+            else:  # or_program_step's transfer: out = r*u_a; u_a -= out; u_b += out
+                out = r * want[a]
+                want[a] = want[a] - out
+                want[b] = want[b] + out
+    got = O.program_step(fields, C5_FLOWS, steps=1000)
+    for g, w in zip(got, want):
+        assert np.max(np.abs(g - w) / np.abs(w)) <= 1e-12
+
+
 def test_step_count_matches_reference_loop(O):
     # SURVEY.md 3.2: fp64 accumulation of src/Model.hpp:48
     assert O.step_count(10.0, 0.2) == 51
