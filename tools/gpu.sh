@@ -26,6 +26,8 @@
 #   bash tools/gpu.sh thin                    segment-plan sweep of the thin split slabs of the
 #                                             c3 N = 8 / N = 4 runs (4096 / 8192 x 32768,
 #                                             self-halo, 200 steps) against the 32768^2 slab
+#   bash tools/gpu.sh thintrace               rocprofv3 kernel traces of the same slabs, split and
+#                                             plain, per pass decomposed (tools/thin_trace.py)
 #   bash tools/gpu.sh scale WL [N...]         the driver's multi-GPU command, N = 1 2 4 8 by
 #                                             default (needs N GPUs; never run on the 1-GPU box)
 #
@@ -169,6 +171,22 @@ thin() {
     done
 }
 
+thintrace() {  # per-pass decomposition of the thin split slabs (tools/thin_trace.py)
+    local steps=${THIN_STEPS:-200} g
+    for g in "4096 32768" "8192 32768"; do
+        set -- $g
+        trace "${1}x${2}_self" c3 $steps 5 --grid $1 $2 --self-halo
+        python3 tools/thin_trace.py "$D/trace_${1}x${2}_self" "${1}x${2} split" \
+            > "$D/trace_${1}x${2}_self/summary.json" && cat "$D/trace_${1}x${2}_self/summary.json"
+        trace "${1}x${2}_plain" c3 $steps 5 --grid $1 $2
+        python3 tools/thin_trace.py "$D/trace_${1}x${2}_plain" "${1}x${2} plain" \
+            > "$D/trace_${1}x${2}_plain/summary.json" && cat "$D/trace_${1}x${2}_plain/summary.json"
+    done
+    trace 32768x32768_plain c3 $steps 5
+    python3 tools/thin_trace.py "$D/trace_32768x32768_plain" "32768x32768 plain" \
+        > "$D/trace_32768x32768_plain/summary.json" && cat "$D/trace_32768x32768_plain/summary.json"
+}
+
 scale() {  # WL [N...]
     local wl=$1
     shift
@@ -194,6 +212,7 @@ case "$cmd" in
     pmc) pmc "$@" ;;
     selfhalo) selfhalo ;;
     thin) thin ;;
+    thintrace) thintrace ;;
     ab) ab "$@" ;;
     final) final ;;
     scale) scale "$@" ;;

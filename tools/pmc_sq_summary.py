@@ -3,7 +3,10 @@
 step kernel: mean counters per dispatch and the wave-cycle split (SQ counters count
 quad-cycles; SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~ SQ_WAVE_CYCLES,
 MI355X_MICROARCH.md 'rocprofv3 PMC slots'), plus the effective clock GRBM_GUI_ACTIVE / 8 XCDs
-/ kernel duration when a kernel-trace average is given."""
+/ kernel duration when a kernel-trace average is given -- only for dispatches of at least
+0.3 ms: GRBM_GUI_ACTIVE counts busy cycles across the dispatch boundaries, so on shorter
+dispatches the quotient reads high (MI355X_MICROARCH.md 'DVFS give-back'; round 5's C2
+figure of 2.59 GHz on 71 us dispatches was above the part's 2.4 GHz maximum)."""
 import csv
 import glob
 import json
@@ -43,7 +46,13 @@ def main():
                 out[key] = out[c] / wc
     if avg_us and "GRBM_GUI_ACTIVE" in out:
         out["kernel_avg_us"] = avg_us
-        out["effective_clock_GHz"] = out["GRBM_GUI_ACTIVE"] / 8.0 / (avg_us * 1e-6) / 1e9
+        clk = out["GRBM_GUI_ACTIVE"] / 8.0 / (avg_us * 1e-6) / 1e9
+        if avg_us >= 300.0:
+            out["effective_clock_GHz"] = clk
+        else:
+            out["effective_clock_GHz"] = None
+            out["effective_clock_note"] = (f"GRBM quotient {clk:.2f} GHz not a clock: dispatch "
+                                           f"{avg_us:.0f} us < 300 us (MI355X_MICROARCH.md DVFS)")
     print(json.dumps(out, indent=1))
 
 
