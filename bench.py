@@ -433,7 +433,7 @@ def main():
     if rank == 0:
         spl = max(plan) if info["kernel"] in (2, 3) and plan else 1
         kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel", 3: "mm_wide_kernel"}[info["kernel"]]
-        traffic = None
+        traffic, traffic_src = None, None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):  # only when it was measured on this kernel
             with open(tf) as f:
@@ -441,6 +441,10 @@ def main():
             key = f"{args.workload}_n{N}_k{spl}"
             if kname in pmc.get(f"{key}_kernel", ""):
                 traffic = pmc.get(f"{key}_bytes_per_launch")
+                # not measured in this run: the PMC passes of tools/gpu.sh prof on this
+                # kernel and workload, recorded by tools/pmc_traffic.py
+                traffic_src = (f"profiles/pmc_traffic.json {key} (rocprofv3 FETCH_SIZE / "
+                               f"WRITE_SIZE passes, {pmc.get(f'{key}_source', 'unrecorded')})")
         lr = None
         if na > 1:  # C5: the program's diffusions and transfers (K = 8: its chain kernel)
             n_diff = sum(1 for f in flows if f[0] == 1)
@@ -455,6 +459,7 @@ def main():
                          cons=abs(s_after - s_before) / abs(s_before), halo=args.halo,
                          self_halo=args.self_halo, lr_cycles=lr,
                          graph_captures_timed=None if host else graphs_timed)
+        line["roofline"]["traffic_source"] = traffic_src
         if args.workload == "c5" and args.program != "c5":
             line["config"]["program"] = f"{args.program}: {flows}"
         if N == 1 and not args.no_cpu_baseline:

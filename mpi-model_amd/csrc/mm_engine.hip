@@ -140,6 +140,9 @@ struct mm_engine {
     std::string graph_note;
 
     bool timing = false;
+    // mm_synchronize polls its streams (hipStreamQuery) before the blocking wait
+    // (MM_SYNC_SPIN=0: the blocking wait alone)
+    bool sync_spin = true;
     std::vector<hipEvent_t> ev_pool;
     std::vector<double> ev_bytes;  // algorithmic bytes of each timed launch (pairs of events)
     size_t ev_used = 0;
@@ -1159,6 +1162,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
     }
     if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
     if (const char* r = std::getenv("MM_CHAIN_RING")) e->ring_ok = std::atoi(r) != 0;
+    if (const char* r = std::getenv("MM_SYNC_SPIN")) e->sync_spin = std::atoi(r) != 0;
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
     // (profiles/r01 sweeps); MM_KERNEL_VARIANT overrides
     e->variant = 2.0 * 8.0 * (double)e->pitch * (double)d.h * d.n_attr > 256.0 * 1048576.0 ? 1 : 0;
@@ -1628,6 +1632,16 @@ int mm_run(mm_engine* e, long long nsteps, long long reduce_every) {
 int mm_synchronize(mm_engine* e) {
     if (!e) return fail(MM_ERR_INVALID, "mm_synchronize: null");
     MM_TRY(set_device(e));
+    if (e->sync_spin) {
+        // poll the completion signals: the blocking wait returns tens to hundreds of us after
+        // the last kernel ends (a sleeping host thread), time the GPU then sits idle in a
+        // timed region or before the next launch
+        for (hipStream_t s : {e->s_comp, e->s_comm}) {
+            hipError_t q;
+            while ((q = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+            if (q != hipSuccess) MM_HIP(q);
+        }
+    }
     MM_HIP(hipStreamSynchronize(e->s_comp));
     MM_HIP(hipStreamSynchronize(e->s_comm));
     return MM_OK;
