@@ -283,6 +283,10 @@ int mm_halo_import(mm_engine* eng, const double* top, const double* bottom);
 /* Test/debug: copy nrows rows starting at local row row0 (owned rows are 0..h-1, ghost
  * rows -kGhost..-1 and h..h+kGhost-1, kGhost = 20) of the current buffer of one attribute to host (W each). */
 int mm_debug_read_rows(mm_engine* eng, int attr, long long row0, long long nrows, double* host);
+/* Test/debug: write `value` into the pitch padding (columns W..pitch-1 of every row, ghost
+ * rows included) of both buffers of every attribute. No result depends on the padding: the
+ * tests poison it with NaN and compare cells and step sums bit for bit. */
+int mm_debug_fill_padding(mm_engine* eng, double value);
 
 /* Measurement: with timing on, mm_run records a HIP event pair around every
  * step-kernel launch on the stream it is launched on; mm_timing returns the

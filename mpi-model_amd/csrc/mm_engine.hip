@@ -1726,6 +1726,23 @@ int mm_debug_read_rows(mm_engine* e, int attr, long long row0, long long nrows, 
     return MM_OK;
 }
 
+int mm_debug_fill_padding(mm_engine* e, double value) {
+    if (!e) return fail(MM_ERR_INVALID, "mm_debug_fill_padding: null");
+    const long long pad = e->pitch - e->d.W;
+    if (pad <= 0) return MM_OK;
+    MM_TRY(set_device(e));
+    MM_HIP(hipStreamSynchronize(e->s_comm));
+    std::vector<double> src((size_t)(pad * e->rows_alloc), value);
+    for (int k = 0; k < 2; ++k)
+        for (int a = 0; a < e->na; ++a)
+            MM_HIP(hipMemcpy2DAsync(e->buf[k][a] - mm::kGhost * e->pitch + e->d.W,
+                                    sizeof(double) * e->pitch, src.data(), sizeof(double) * pad,
+                                    sizeof(double) * pad, e->rows_alloc, hipMemcpyHostToDevice,
+                                    e->s_comp));
+    MM_HIP(hipStreamSynchronize(e->s_comp));
+    return MM_OK;
+}
+
 int mm_set_timing(mm_engine* e, int on) {
     if (!e) return fail(MM_ERR_INVALID, "mm_set_timing: null");
     MM_TRY(set_device(e));

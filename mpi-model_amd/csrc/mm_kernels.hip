@@ -172,14 +172,15 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
         }
         return;
     }
-    // (sx == 0: a row outside the global grid weighs 0)
+    // (sx == 0: a row outside the global grid weighs 0; a column outside it -- the pitch
+    // padding -- weighs 0 by select, so no value it holds reaches a cell)
     const double c0 = c8_one(sx * sy0 - 1), c1 = c8_one(sx * sy1 - 1), ce = c8_one(sx * sye - 1);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         const bool dif = A.diffuse_mask & (1 << a);
-        o.w0[a] = dif ? u0[a] * c0 : 0.0;
-        o.w1[a] = dif ? u1[a] * c1 : 0.0;
-        o.we[a] = dif ? ue[a] * ce : 0.0;
+        o.w0[a] = (dif && sy0) ? u0[a] * c0 : 0.0;
+        o.w1[a] = (dif && sy1) ? u1[a] * c1 : 0.0;
+        o.we[a] = (dif && sye) ? ue[a] * ce : 0.0;
     }
 }
 

@@ -256,9 +256,10 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
         } else if (inner) {  // interior row, interior strip: cnt == 8, w = u
             w0[a] = u0[a];
             w1[a] = u1[a];
-        } else {
-            w0[a] = u0[a] * c8k(sx * c.sy0 - 1);
-            w1[a] = u1[a] * c8k(sx * c.sy1 - 1);
+        } else {  // a column outside the grid (span 0: its pitch padding) weighs 0 by select,
+                  // so no value it holds reaches a cell
+            w0[a] = c.sy0 == 0 ? 0.0 : u0[a] * c8k(sx * c.sy0 - 1);
+            w1[a] = c.sy1 == 0 ? 0.0 : u1[a] * c8k(sx * c.sy1 - 1);
         }
     }
 }

@@ -504,6 +504,17 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
 #endif
             }
         }
+        if (BODY == kBodyGen) {
+            // the GEN body weights every column by its own count, 0 outside the grid
+            // (w = u * 0): a column past the grid enters as 0, whatever the pitch padding
+            // holds, as the OOB loads left of the grid do (EDGE / FAST rows keep such
+            // columns out of the grid at the DPP hand-off instead)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+#pragma unroll
+                for (int k = 0; k < C; ++k) cur[a][k] = x.c.sy[k] == 0 ? 0.0 : cur[a][k];
+            }
+        }
         const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -739,10 +750,17 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
     }
     wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
     if (RED) {
+        // the OWNED groups add fma(o, 0, acc) in the columns a lane does not own: lanes that
+        // own none (halo lanes, lanes past the grid, which read the pitch padding) leave the
+        // sum here, so no value they hold can reach it. The padding columns inside the
+        // grid's last lane (W % C != 0) hold only what this kernel stored there: zero at
+        // creation (mm_engine_create), host copies write W columns.
+        const bool lane_owns = x.c.own[0];
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
 #pragma unroll
-            for (int a = 0; a < NA; ++a) carry[q][a] = carry[q][a] + wave_sum_k(st.acc[q][a]);
+            for (int a = 0; a < NA; ++a)
+                carry[q][a] = carry[q][a] + wave_sum_k(lane_owns ? st.acc[q][a] : 0.0);
         }
     }
 }

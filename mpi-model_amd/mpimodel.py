@@ -35,7 +35,7 @@ EXPORTS = [
     "mm_engine_info", "mm_fill", "mm_upload", "mm_download", "mm_clear_flows", "mm_add_flow",
     "mm_point_apply", "mm_run", "mm_prepare", "mm_pass_plan", "mm_pass_kernel", "mm_synchronize", "mm_sums", "mm_sums_history",
     "mm_clear_history", "mm_halo_export_rows", "mm_halo_import_rows", "mm_halo_export",
-    "mm_halo_import", "mm_debug_read_rows",
+    "mm_halo_import", "mm_debug_read_rows", "mm_debug_fill_padding",
     "mm_set_timing", "mm_timing", "mm_partition_rect_reference", "mm_owner_rect_reference",
     "mm_wire_format_partition", "mm_wire_format_flow", "mm_wire_parse_partition",
     "mm_wire_parse_flow", "mm_point_strict_applies", "mm_point_apply_strict",
@@ -117,6 +117,7 @@ def lib():
             "mm_halo_export": (I, [P, P, P]),
             "mm_halo_import": (I, [P, P, P]),
             "mm_debug_read_rows": (I, [P, I, LL, LL, P]),
+            "mm_debug_fill_padding": (I, [P, D]),
             "mm_set_timing": (I, [P, I]),
             "mm_partition_rect_reference": (I, [I, I, I, I, I, pI, pI, pI, pI]),
             "mm_point_strict_applies": (I, [I, I, I, I, I]),
@@ -383,6 +384,10 @@ class Engine:
         out = np.empty((nrows, self.W), dtype=np.float64)
         check(lib().mm_debug_read_rows(self.ptr, attr, row0, nrows, _dptr(out)))
         return out
+
+    def fill_padding(self, value):
+        """Test hook: write value into every row's pitch padding (columns W..pitch-1)."""
+        check(lib().mm_debug_fill_padding(self.ptr, float(value)))
 
     def set_timing(self, on):
         check(lib().mm_set_timing(self.ptr, 1 if on else 0))
