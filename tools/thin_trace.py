@@ -59,20 +59,26 @@ def main():
     passes = []
     for i, it in enumerate(interior):
         nxt = interior[i + 1] if i + 1 < len(interior) else None
-        lo = it["t0"] - 1e9 if i == 0 else interior[i - 1]["t1"]
+        # border k is launched beside interior k (the two streams start together): the
+        # border launch whose start is nearest this interior's; exchange k+1 follows it on
+        # the comm stream (the RCCL kernels between that border's end and the next
+        # interior's start)
+        b = min(border, key=lambda r: abs(r["t0"] - it["t0"])) if border else None
+        if b is not None and abs(b["t0"] - it["t0"]) > 100.0:
+            b = None
         hi = nxt["t0"] if nxt else it["t1"] + 1e9
-        # border k starts after interior k-1 ended and before interior k+1 starts
-        b = [r for r in border if lo <= r["t0"] < hi]
-        # exchange k: the RCCL kernels that end before border k starts, after border k-1
-        e = [r for r in rccl if (b[0]["t0"] if b else hi) >= r["t1"] > lo - (it["t1"] - it["t0"])] if rccl else []
+        e = [r for r in rccl if b is not None and b["t1"] <= r["t0"] < hi]
         rec = {
             "interior_us": it["t1"] - it["t0"],
             "interior_grid": it["grid"],
-            "border_us": sum(r["t1"] - r["t0"] for r in b) if b else None,
+            "border_us": (b["t1"] - b["t0"]) if b else None,
             "exchange_us": sum(r["t1"] - r["t0"] for r in e) if e else None,
             "gap_after_interior_us": (nxt["t0"] - it["t1"]) if nxt else None,
             "period_us": (nxt["t0"] - it["t0"]) if nxt else None,
-            "border_end_after_interior_end_us": (b[-1]["t1"] - it["t1"]) if b else None,
+            # the comm stream's work of the pass (border, then the next exchange) ends this
+            # long before (< 0) or after the interior kernel
+            "comm_end_minus_interior_end_us": ((max([b["t1"]] + [r["t1"] for r in e]) - it["t1"])
+                                               if b else None),
         }
         passes.append(rec)
     # steady passes: drop the cold first pass of each back-to-back run (a gap > 1 ms)
@@ -81,7 +87,7 @@ def main():
               and passes[i - 1]["gap_after_interior_us"] < 1000 and p["period_us"] is not None]
     out = {"label": label, "passes": len(passes), "steady_passes": len(steady)}
     for k in ("interior_us", "border_us", "exchange_us", "gap_after_interior_us", "period_us",
-              "border_end_after_interior_end_us"):
+              "comm_end_minus_interior_end_us"):
         out[k + "_median"] = med([p[k] for p in steady if p[k] is not None])
     if steady and out["period_us_median"]:
         out["interior_share_of_period"] = round(out["interior_us_median"] / out["period_us_median"], 4)
