@@ -184,14 +184,16 @@ def cpu_baseline_program(H, W, na, flows, seconds):
 
 def level_row_cycles(cols, n_diffuse=1, n_transfers=0, chain_kernel=0):
     """VALU cycles one wave issues per level-row of its strip: per diffusing
-    attribute 6 fp64 instructions per column of a lane (4 cycles each on a SIMD: the
-    per-receiver step of oracle/mm_oracle.h, 2 adds vertical, 2 horizontal, 2 fma) and the
-    two fp64 DPP neighbour moves (4 v_mov_dpp, 2 cycles each); per transfer of a chain and
+    attribute 5 fp64 instructions per column of a lane on average (4 cycles each on a SIMD:
+    the box-sum step of oracle/mm_oracle.h -- the column triple 2 adds on an even row, 1 on
+    the odd row after it, which reuses the pair's sum; the box sum 1.5 adds, the lane's
+    columns paired alike; 2 fma) and the two fp64 DPP neighbour moves (4 v_mov_dpp, 2 cycles
+    each); per transfer of a chain and
     column, 3 fp64 instructions (out = r*u_a, u_a - out, u_b + out) -- with compile-time
     operands (mm.MM_CHAIN_RING) and with chain_asm's run-time operands (mm.MM_CHAIN_RUNTIME)
     alike: chain_asm indexes the fp64 instructions' own operands, no moves."""
     del chain_kernel  # both chain kernels issue the same instructions per transfer
-    diff = n_diffuse * (6 * cols * 4 + 4 * 2)
+    diff = n_diffuse * (5 * cols * 4 + 4 * 2)
     return diff + n_transfers * cols * 3 * 4
 
 

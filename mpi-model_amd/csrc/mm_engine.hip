@@ -490,15 +490,18 @@ void seg_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lon
     const long long maxr = std::max<long long>(16, mm::passk_max_rows(k, e->pitch));
     const double edge = seg_edge_of(e, k);
     const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
+    // even segment lengths: with an even first row (x_init and lo even, as every bench
+    // slab) no segment pays the odd-start shift of the row-paired kernels (one extra row)
+    auto even_rows = [&](long long rr) { return std::min(maxr & ~1LL, rr + (rr & 1)); };
     auto re_of = [&](long long rr) {
-        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
+        return even_rows(std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge))));
     };
     auto plan = [&](double sw) {
         const long long want = std::max<long long>(1, (long long)(sw * e->ncu * wpc));
         long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
         r = std::min(std::max<long long>(r, 16), maxr);
         while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
-        return std::min(r, maxr);
+        return even_rows(std::min(r, maxr));
     };
     long long r;
     if (e->seg_waves > 0.0) {
@@ -582,15 +585,18 @@ void wide_range(mm_engine* e, int k, bool red, mm::PassArgs& A, long long lo, lo
     // full length; profiles/r05/edge)
     const double edge = e->seg_edge > 0.0 ? e->seg_edge : (e->na == 1 ? 1.0 : 0.5);
     const double units = ns < 3 ? (double)ns / edge : (double)(ns - 2) + 2.0 / edge;
+    // even segment lengths: with an even first row (x_init and lo even, as every bench
+    // slab) no segment pays the odd-start shift of the row-paired kernels (one extra row)
+    auto even_rows = [&](long long rr) { return std::min(maxr & ~1LL, rr + (rr & 1)); };
     auto re_of = [&](long long rr) {
-        return std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge)));
+        return even_rows(std::min(maxr, std::max<long long>(8, (long long)((double)rr * edge))));
     };
     auto plan = [&](double sw) {
         const long long want = std::max<long long>(1, (long long)(sw * e->ncu * bpc));
         long long r = (long long)std::ceil((double)std::max<long long>(n, 1) * units / (double)want);
         r = std::min(std::max<long long>(r, 16), maxr);
         while (r < maxr && seg_wave_count(n, ns, r, re_of(r)) > want) r += std::max<long long>(1, r / 64);
-        return std::min(r, maxr);
+        return even_rows(std::min(r, maxr));
     };
     long long r;
     if (e->seg_waves > 0.0) {
@@ -1511,20 +1517,31 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
         e->cur = cur0;
         MM_HIP(hipStreamSynchronize(e->s_comp));
     }
-    // the eagerly launched passes: plan them now, which loads their kernels' code objects
+    // the eagerly launched passes: plan them now, which loads their kernels' code objects,
+    // and dispatch each planned kernel once with no work (every workgroup leaves at its
+    // first instruction: waves_total = 0), so the queue's scratch is sized for it here and
+    // not by the first timed pass (the K = 20 kernel keeps a few hundred bytes of scratch
+    // per lane in its GEN code: its first dispatch started 172 us after its launch,
+    // profiles/r06/hiptrace). No step runs: no buffer is read or written.
     if (passk_ok(e) && tail > 0) {
+        const bool red = reduce_every > 0;
         for (long long s = 0, k = 0; s < tail; s += k) {
             k = next_pass_len(e, tail - s);
             mm::PassArgs A;
             std::memset(&A, 0, sizeof A);
-            if (use_wide(e, (int)k)) {
+            const bool wide = use_wide(e, (int)k);
+            if (wide) {
                 A.nstrips = (int)nstrips_wide(e, (int)k);
-                wide_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
+                wide_range(e, (int)k, red, A, 0, e->d.h);
             } else {
                 A.nstrips = (int)nstrips_k(e, (int)k);
-                seg_range(e, (int)k, reduce_every > 0, A, 0, e->d.h);
+                seg_range(e, (int)k, red, A, 0, e->d.h);
             }
+            A.waves_total = 0;
+            A.waves_a = -1;  // the priming mark (mm::launch_passk / launch_wide)
+            MM_TRY(launch_timed(e, red, A, 0, false, wide ? -(int)k : (int)k));
         }
+        MM_HIP(hipStreamSynchronize(e->s_comp));
     }
     return MM_OK;
 }

@@ -62,6 +62,15 @@ __device__ __forceinline__ double c8_one(int cnt) {
                                             : (cnt == 2 ? 4.0 : (cnt == 1 ? 8.0 : 0.0))));
 }
 
+// The own-weight coefficient of the box sum (oracle/mm_oracle.c m_of): -(8 + 8/cnt), 0 for a
+// cell without neighbours (it keeps its value) or outside the grid.
+__device__ __forceinline__ double m8_one(int cnt) {
+    return cnt == 8 ? -9.0
+                    : (cnt == 5 ? -(8.0 + 8.0 / 5.0)
+                                : (cnt == 3 ? -(8.0 + 8.0 / 3.0)
+                                            : (cnt == 2 ? -12.0 : (cnt == 1 ? -16.0 : 0.0))));
+}
+
 // Chain entries are read with compile-time indices only, so they are scalar loads of
 // the kernel arguments that the compiler hoists out of the row loop (a runtime index
 // into the by-value PassArgs turns into per-row global loads and vmcnt(0) waits that
@@ -95,8 +104,8 @@ struct RawRow {
     double v0[NA], v1[NA], ve[NA];
 };
 
-// Processed row: weights (three columns), values and the self coefficient (-8, or 0 for a
-// cell without neighbours) of the two own columns.
+// Processed row: weights (three columns), values and the own-weight coefficient
+// -(8 + 8/cnt) of the box sum (0 for a cell without neighbours) of the two own columns.
 template <int NA>
 struct ProcRow {
     double w0[NA], w1[NA], we[NA];
@@ -155,8 +164,8 @@ __device__ __forceinline__ void process_row(const PassArgs& A, int r, const RawR
         apply_chain<NA>(u1, A.npre, A.pre_a, A.pre_b, A.pre_r);
         apply_chain<NA>(ue, A.npre, A.pre_a, A.pre_b, A.pre_r);
     }
-    o.m0 = (sx && sx * sy0 == 1) ? 0.0 : -8.0;
-    o.m1 = (sx && sx * sy1 == 1) ? 0.0 : -8.0;
+    o.m0 = m8_one(sx * sy0 - 1);
+    o.m1 = m8_one(sx * sy1 - 1);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         o.u0[a] = u0[a];
@@ -190,20 +199,29 @@ __device__ __forceinline__ void emit_row(const PassArgs& A, int r, int rmax, uns
                                          const ProcRow<NA>& C, const ProcRow<NA>& N,
                                          double (&acc)[NA]) {
     double w0[NA], w1[NA];
+    // the column triples pair the rows from an even global row: row x even
+    // w(x-1) + (w(x) + w(x+1)), odd (w(x-1) + w(x)) + w(x+1) (wave-uniform branch)
+    const bool even = ((A.x_init + r) & 1) == 0;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         if (A.diffuse_mask & (1 << a)) {
-            const double p0 = P.w0[a] + N.w0[a];
-            const double p1 = P.w1[a] + N.w1[a];
-            const double pe = P.we[a] + N.we[a];
-            const double c0 = p0 + C.w0[a];
-            const double c1 = p1 + C.w1[a];
-            const double ce = pe + C.we[a];
+            double c0, c1, ce;
+            if (even) {
+                c0 = P.w0[a] + (C.w0[a] + N.w0[a]);
+                c1 = P.w1[a] + (C.w1[a] + N.w1[a]);
+                ce = P.we[a] + (C.we[a] + N.we[a]);
+            } else {
+                c0 = (P.w0[a] + C.w0[a]) + N.w0[a];
+                c1 = (P.w1[a] + C.w1[a]) + N.w1[a];
+                ce = (P.we[a] + C.we[a]) + N.we[a];
+            }
             const double left = dpp_from_lower_lane(c1, ce);   // cw at column y0-1
             const double right = dpp_from_upper_lane(c0, ce);  // cw at column y0+2
             const double r8 = A.drate[a] * 0.125;
-            w0[a] = __builtin_fma(__builtin_fma(C.u0[a], C.m0, (left + c1) + p0), r8, C.u0[a]);
-            w1[a] = __builtin_fma(__builtin_fma(C.u1[a], C.m1, (c0 + right) + p1), r8, C.u1[a]);
+            // the box sums of the lane's even and odd column (columns paired from y0)
+            const double pk = c0 + c1;
+            w0[a] = __builtin_fma(__builtin_fma(C.u0[a], C.m0, left + pk), r8, C.u0[a]);
+            w1[a] = __builtin_fma(__builtin_fma(C.u1[a], C.m1, pk + right), r8, C.u1[a]);
         } else {
             w0[a] = C.u0[a];
             w1[a] = C.u1[a];

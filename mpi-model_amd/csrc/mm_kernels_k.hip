@@ -89,8 +89,11 @@ int passk_waves_per_cu(int k, int na, bool red, int nt) {
     }
 }
 
+// A pass of no work is not launched -- unless waves_a < 0 marks it as mm_prepare's
+// priming dispatch: one workgroup that leaves at its first instruction (waves_total = 0),
+// which loads the kernel and sizes the queue's scratch for it ahead of the run.
 hipError_t launch_passk(int k, int na, bool red, const PassArgs& a, hipStream_t s, int variant) {
-    if (a.waves_total <= 0) return hipSuccess;
+    if (a.waves_total <= 0 && a.waves_a >= 0) return hipSuccess;
     switch (k) {
         case 1: return passk_launch_k1(na, red, a, s, variant);
         case 2: return passk_launch_k2(na, red, a, s, variant);
@@ -164,7 +167,7 @@ int wide_blocks_per_cu(int k, int c, int na, bool red, int nt) {
 
 hipError_t launch_wide(int k, int c, int na, bool red, const PassArgs& a, hipStream_t s,
                        int variant) {
-    if (a.waves_total <= 0) return hipSuccess;
+    if (a.waves_total <= 0 && a.waves_a >= 0) return hipSuccess;  // (waves_a < 0: priming)
     if (!wide_has(k, c, na)) return hipErrorInvalidValue;
     if (na > 1 && k == 8 && (variant & 2)) return widear_launch_k8(na, red, a, s, variant & 1);
     if (na > 1 && k == 4) return widea_launch_k4(na, red, a, s, variant & 1);

@@ -37,9 +37,9 @@
 //   * BLOCK: 4 rows, fully unrolled -- the border rows of a halo-split pass.
 //
 // Every level uses exactly the single-step arithmetic of oracle/mm_oracle.h (transfers
-// in declared order, then per emitter s = out/cnt and d = u - out -- for cnt == 8 as
-// s = u*(r/8), d = fma(s, -8, u) -- and v' = d + nb), so K fused steps are bit-identical
-// to K single steps (built with -ffp-contract=off; the one fma is explicit).
+// in declared order, then the weights w = u * 8/cnt, the row-paired column triples, the
+// column-paired box sum S and v' = fma(fma(u, -(8 + 8/cnt), S), r/8, u)), so K fused steps
+// are bit-identical to K single steps (built with -ffp-contract=off; the fma explicit).
 //
 // This header holds the kernel templates; mm_passk_k<K>.hip instantiate them (one
 // translation unit per K so the builds run in parallel) and mm_kernels_k.hip dispatches.
@@ -161,6 +161,17 @@ __device__ __forceinline__ double c8k(int cnt) {
                                             : (cnt == 2 ? 4.0 : (cnt == 1 ? 8.0 : 0.0))));
 }
 
+// The own-weight coefficient -(8 + 8/cnt) of the box sum (oracle/mm_oracle.c m_of): -9 for
+// an interior cell, 0 for a cell without neighbours (it keeps its value) or outside the grid.
+constexpr double kM8 = -9.0;
+constexpr double kM5 = -(8.0 + 8.0 / 5.0);
+__device__ __forceinline__ double m8k(int cnt) {
+    return cnt == 8 ? kM8
+                    : (cnt == 5 ? kM5
+                                : (cnt == 3 ? -(8.0 + 8.0 / 3.0)
+                                            : (cnt == 2 ? -12.0 : (cnt == 1 ? -16.0 : 0.0))));
+}
+
 // Descriptor of `rows` consecutive rows starting at `first` (pointer already offset):
 // row k of the range is at byte offset k*pitch*8 (added to the lane's voffset), offsets
 // past the range -- later rows, or lanes whose voffset is kOOBk -- load 0 / drop stores.
@@ -190,8 +201,9 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, unsigned off
                                            (NT & 1) ? 2 : 0);
 }
 
-// One level's three-row window of one attribute: the weights of the row above (wa) and of
-// the current row (wm), the current row's values (um).
+// One level's three-row window of one attribute: the weights of the row above (wa; before
+// an odd row is emitted, the pair sum of the row above and the current row) and of the
+// current row (wm), the current row's values (um).
 struct Win {
     double wa0, wa1, wm0, wm1, um0, um1;
 };
@@ -264,10 +276,12 @@ __device__ __forceinline__ void proc_n(const PassArgs& A, const Lane& c, long lo
     }
 }
 
-// Level input row m = 0 or 1 (global row gx): fill the windows.
+// Level input row m = 0 or 1 (global row gx): fill the windows. e1: parity of the level's
+// first emitted row (row gx at m = 1): odd, the window holds the pair sum of rows m = 0, 1.
 template <int NA, bool FAST, bool CHAIN>
 __device__ __forceinline__ void level_fill(const PassArgs& A, const Lane& c, long long gx, int m,
-                                           Win (&w)[NA], double (&u0)[NA], double (&u1)[NA]) {
+                                           int e1, Win (&w)[NA], double (&u0)[NA],
+                                           double (&u1)[NA]) {
     double w0[NA], w1[NA];
     proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, w0, w1);
 #pragma unroll
@@ -276,6 +290,10 @@ __device__ __forceinline__ void level_fill(const PassArgs& A, const Lane& c, lon
             w[a].wa0 = w0[a];
             w[a].wa1 = w1[a];
         } else {
+            if (e1) {
+                w[a].wa0 = w[a].wa0 + w0[a];
+                w[a].wa1 = w[a].wa1 + w1[a];
+            }
             w[a].wm0 = w0[a];
             w[a].wm1 = w1[a];
             w[a].um0 = u0[a];
@@ -285,27 +303,43 @@ __device__ __forceinline__ void level_fill(const PassArgs& A, const Lane& c, lon
 }
 
 // Level input row m >= 2 (global row gx): emit the windows' current row (then the
-// post-chain) and slide the windows.
-// v' = fma(fma(u, -8, W8), r/8, u), W8 = (cw(y-1) + cw(y+1)) + pw with pw = w(x-1) + w(x+1)
-// and cw = pw + w(x) (src/Model.hpp:206-211,234; the order fixed by oracle/mm_oracle.h); a
-// cell without neighbours (a 1 x 1 grid) keeps its value.
+// post-chain) and slide the windows. e: parity of the emitted row gx - 1 (a constant where
+// the iteration is unrolled). Even: the pair sum of this row and the next, p = wm + wn,
+// gives the column triple wa + p and stays in wa for the odd row after it, whose triple is
+// p + wn; the box sum of the lane's even / odd column: cw(y-1) + (cw(y) + cw(y+1)) /
+// (cw(y-1) + cw(y)) + cw(y+1); v' = fma(fma(u, -(8 + 8/cnt), S), r/8, u)
+// (src/Model.hpp:206-211,234; the order fixed by oracle/mm_oracle.h); a cell without
+// neighbours (a 1 x 1 grid) keeps its value.
 template <int NA, bool FAST, bool CHAIN>
-__device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, long long gx,
+__device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, long long gx, int e,
                                            Win (&w)[NA], double (&u0)[NA], double (&u1)[NA],
                                            double (&o0)[NA], double (&o1)[NA]) {
     double wn0[NA], wn1[NA];
     proc_n<NA, FAST, CHAIN>(A, c, gx, u0, u1, wn0, wn1);
     const int sxm = FAST ? 3 : span3k(c.H, gx - 1);  // the emitted row
-    const double m0 = (!FAST && sxm * c.sy0 == 1) ? 0.0 : -8.0;
-    const double m1 = (!FAST && sxm * c.sy1 == 1) ? 0.0 : -8.0;
+    const double m0 = FAST ? kM8 : m8k(sxm * c.sy0 - 1);
+    const double m1 = FAST ? kM8 : m8k(sxm * c.sy1 - 1);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
+        double na0, na1;  // the window's next wa
         if (NA > 1 && !((A.diffuse_mask >> a) & 1)) {
             o0[a] = w[a].um0;
             o1[a] = w[a].um1;
+            na0 = w[a].wm0;
+            na1 = w[a].wm1;
         } else {
-            const double p0 = w[a].wa0 + wn0[a], p1 = w[a].wa1 + wn1[a];
-            const double c0 = p0 + w[a].wm0, c1 = p1 + w[a].wm1;
+            double c0, c1;
+            if (e == 0) {
+                na0 = w[a].wm0 + wn0[a];
+                na1 = w[a].wm1 + wn1[a];
+                c0 = w[a].wa0 + na0;
+                c1 = w[a].wa1 + na1;
+            } else {
+                c0 = w[a].wa0 + wn0[a];
+                c1 = w[a].wa1 + wn1[a];
+                na0 = w[a].wm0;
+                na1 = w[a].wm1;
+            }
 #if MM_SHIFT_LDS
             const double left = lds_shift(c1, c.from_lower);
             const double right = lds_shift(c0, c.from_upper);
@@ -314,11 +348,12 @@ __device__ __forceinline__ void level_emit(const PassArgs& A, const Lane& c, lon
             const double right = dpp_upper(c0);  // cw at column y0+2 (lane+1's first column)
 #endif
             const double r8 = A.drate[a] * 0.125;
-            o0[a] = __builtin_fma(__builtin_fma(w[a].um0, m0, (left + c1) + p0), r8, w[a].um0);
-            o1[a] = __builtin_fma(__builtin_fma(w[a].um1, m1, (c0 + right) + p1), r8, w[a].um1);
+            const double pk = c0 + c1;
+            o0[a] = __builtin_fma(__builtin_fma(w[a].um0, m0, left + pk), r8, w[a].um0);
+            o1[a] = __builtin_fma(__builtin_fma(w[a].um1, m1, pk + right), r8, w[a].um1);
         }
-        w[a].wa0 = w[a].wm0;
-        w[a].wa1 = w[a].wm1;
+        w[a].wa0 = na0;
+        w[a].wa1 = na1;
         w[a].wm0 = wn0[a];
         w[a].wm1 = wn1[a];
         w[a].um0 = u0[a];
@@ -371,8 +406,9 @@ struct Bufs {
 };
 
 // BLOCK schedule: TH rows, every iteration unrolled at compile time (level fill states,
-// row offsets and block ownership are all constants).
-template <int K, int TH, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
+// row offsets, block ownership and, per GP = the parity of the first input row, the rows'
+// parities are all constants).
+template <int K, int TH, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN, int GP>
 __device__ __forceinline__ void passk_block(const PassArgs& A, const Lane& c, long long wid,
                                             int lane, int rA, int rB, unsigned voff,
                                             unsigned soff) {
@@ -413,11 +449,11 @@ __device__ __forceinline__ void passk_block(const PassArgs& A, const Lane& c, lo
             }
             const long long gx = c.gx0 + rA - K + (j - 1) + m;
             if (m < 2) {
-                level_fill<NA, FAST, CHAIN>(A, c, gx, m, win[j - 1], u0, u1);
+                level_fill<NA, FAST, CHAIN>(A, c, gx, m, (GP + j) & 1, win[j - 1], u0, u1);
                 continue;
             }
             double w0[NA], w1[NA];
-            level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
+            level_emit<NA, FAST, CHAIN>(A, c, gx, (GP + j + m) & 1, win[j - 1], u0, u1, w0, w1);
             const int orow = m + j - K - 2;  // output row - rA (compile-time)
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
@@ -439,13 +475,17 @@ __device__ __forceinline__ void passk_block(const PassArgs& A, const Lane& c, lo
 // Steady state of the SEGMENT schedule, iterations [b0, b1) (b0 = I0 mod U): every level
 // emits one row per iteration, level K's row rA + (i - I0) is stored. FAST: every row the
 // levels read in these iterations is an interior row of an interior strip.
+// rG: the segment's geometry start (rA, or rA - 1 for a shifted segment, passk_segment),
+// whose first input row is even: level j's row emitted at iteration i, rG - K - 2j + 1 + i,
+// has the parity of i + 1.
 template <int K, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
 __device__ __forceinline__ void seg_steady(const PassArgs& A, const Lane& c, const Bufs<K, NA>& B,
-                                           int rA, int rB, unsigned voff, unsigned soff,
+                                           int rG, int rA, int rB, unsigned voff, unsigned soff,
                                            unsigned rowb, int b0, int b1, dv2 (&raw)[U][NA],
                                            Win (&win)[K][NA], double (&pend0)[K][NA],
                                            double (&pend1)[K][NA], double (&acc)[K][NA]) {
     constexpr int I0 = 3 * K - 1;
+    const __amdgpu_buffer_rsrc_t none = rows_rsrc(A.out[0], 0, A.pitch);
     for (int base = b0; base < b1; base += U) {
 #pragma unroll
         for (int t = 0; t < U; ++t) {
@@ -470,15 +510,21 @@ __device__ __forceinline__ void seg_steady(const PassArgs& A, const Lane& c, con
                         u1[a] = pend1[j - 2][a];
                     }
                 }
-                const long long gx = c.gx0 + rA - K + i - 2 * (j - 1);
+                const long long gx = c.gx0 + rG - K + i - 2 * (j - 1);
                 double w0[NA], w1[NA];
-                level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-                const int r = rA - K - 2 * j + 1 + i;  // output row
+                // an even U keeps base = I0 (mod 2): the parity is a constant per unrolled
+                // row; an odd U (the 3- / 4-attribute K = 1, 2 instances) reads it at run time
+                const int e = U % 2 == 0 ? (I0 + t + 1) & 1 : (i + 1) & 1;
+                level_emit<NA, FAST, CHAIN>(A, c, gx, e, win[j - 1], u0, u1, w0, w1);
+                const int r = rG - K - 2 * j + 1 + i;  // output row
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
                     if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
                     if (j == K) {
-                        store_row<NT>(B.out[a], soff + (unsigned)(i - I0) * rowb, w0[a], w1[a]);
+                        // row r of out (base rA); a shifted segment's row rA - 1 is dropped
+                        const int ro = r - rA;
+                        store_row<NT>(ro < 0 ? none : B.out[a], soff + (unsigned)(ro < 0 ? 0 : ro) * rowb,
+                                      w0[a], w1[a]);
                     } else {
                         pend0[j - 1][a] = w0[a];
                         pend1[j - 1][a] = w1[a];
@@ -503,12 +549,19 @@ __device__ __forceinline__ void seg_steady(const PassArgs& A, const Lane& c, con
 // A wave of an interior strip whose segment touches the grid's first or last rows runs
 // the general body only for the iterations that read those rows and the branch-free body
 // in between (the general body's per-row branches keep the K levels from interleaving).
+// Rows are paired from an even global row (level_emit): a segment whose first input row
+// gx0 + rA - K is odd starts one row higher (rG = rA - 1) -- an extra first input row that
+// loads as 0 (row -1 of the input descriptor: its offset wraps past num_records) and an
+// extra first output row that is not stored or summed (its value depends on that 0 row;
+// the rows below it do not).
 template <int K, int U, bool RED, int NT, bool FAST, int NA, bool CHAIN>
 __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, long long wid,
                                               int lane, int rA, int rB, unsigned voff,
                                               unsigned soff) {
     constexpr int I0 = 3 * K - 1;
-    const int R = rB - rA;
+    const int sh = (int)((c.gx0 + rA - K) & 1);
+    const int rG = rA - sh;
+    const int R = rB - rG;
     double acc[K][NA];
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -516,6 +569,7 @@ __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, 
         for (int a = 0; a < NA; ++a) acc[j][a] = 0.0;
     const unsigned rowb = (unsigned)(A.pitch * 8);
     const Bufs<K, NA> B(A, rA, rB);
+    voff -= (unsigned)sh * rowb;  // input row k of the segment: row k - sh of B.in
     dv2 raw[U][NA];
 #pragma unroll
     for (int k = 0; k < U; ++k)
@@ -543,14 +597,14 @@ __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, 
                     u1[a] = pend1[j - 2][a];
                 }
             }
-            const long long gx = c.gx0 + rA - K + (j - 1) + m;
+            const long long gx = c.gx0 + rG - K + (j - 1) + m;
             if (m < 2) {
-                level_fill<NA, FAST, CHAIN>(A, c, gx, m, win[j - 1], u0, u1);
+                level_fill<NA, FAST, CHAIN>(A, c, gx, m, j & 1, win[j - 1], u0, u1);
                 continue;
             }
             double w0[NA], w1[NA];
-            level_emit<NA, FAST, CHAIN>(A, c, gx, win[j - 1], u0, u1, w0, w1);
-            const int r = rA - K - 2 * j + 1 + i;  // output row
+            level_emit<NA, FAST, CHAIN>(A, c, gx, (j + m) & 1, win[j - 1], u0, u1, w0, w1);
+            const int r = rG - K - 2 * j + 1 + i;  // output row
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 if (RED) accum(acc[j - 1][a], r >= rA && r < rB, c, w0[a], w1[a]);
@@ -563,26 +617,28 @@ __device__ __forceinline__ void passk_segment(const PassArgs& A, const Lane& c, 
 
     const int end = I0 + (R + U - 1) / U * U;
     if (FAST) {
-        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, I0, end,
+        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rG, rA, rB, voff, soff, rowb, I0, end,
                                                    raw, win, pend0, pend1, acc);
     } else {
         int f0 = end, f1 = end;  // iterations [f0, f1) read interior rows only
         if (c.fast_cols) {
-            // iteration i: the levels read global rows g - 2(K-1) .. g, g = gx0 + rA - K + i
-            const long long g0 = c.gx0 + rA - K;
-            const long long lo = 1 + 2 * (K - 1) - g0;  // first i with every row >= 1
+            // iteration i: the levels read global rows g - 2(K-1) .. g, g = gx0 + rG - K + i,
+            // and emit the rows before them, whose own-weight coefficient the FAST body
+            // takes as the interior's (-9): every row read >= 2
+            const long long g0 = c.gx0 + rG - K;
+            const long long lo = 2 + 2 * (K - 1) - g0;  // first i with every row >= 2
             const long long hi = c.H - 1 - g0;          // first i with a row > H-2
             const long long a0 = lo <= I0 ? I0 : I0 + (lo - I0 + U - 1) / U * U;
             const long long a1 = hi <= I0 ? I0 : I0 + (hi - I0) / U * U;
             f0 = (int)min((long long)end, a0);
             f1 = (int)max((long long)f0, min((long long)end, a1));
         }
-        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, I0, f0,
-                                                    raw, win, pend0, pend1, acc);
-        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, f0, f1,
+        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rG, rA, rB, voff, soff, rowb, I0,
+                                                    f0, raw, win, pend0, pend1, acc);
+        seg_steady<K, U, RED, NT, true, NA, CHAIN>(A, c, B, rG, rA, rB, voff, soff, rowb, f0, f1,
                                                    raw, win, pend0, pend1, acc);
-        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rA, rB, voff, soff, rowb, f1, end,
-                                                    raw, win, pend0, pend1, acc);
+        seg_steady<K, U, RED, NT, false, NA, CHAIN>(A, c, B, rG, rA, rB, voff, soff, rowb, f1,
+                                                    end, raw, win, pend0, pend1, acc);
     }
     if (RED) write_sums<K, NA>(A, wid, lane, acc);
 }
@@ -692,17 +748,25 @@ __global__ __launch_bounds__(kBlock, MM_PASSK_MIN_WAVES) void mm_passk_kernel(co
         else
             passk_segment<K, U, RED, NT, false, NA, CHAIN>(A, c, wid, lane, rA, rB, voff, soff);
     } else {
-        if (fast)
-            passk_block<K, MODE, U, RED, NT, true, NA, CHAIN>(A, c, wid, lane, rA, rB, voff, soff);
+        // the block's rows' parities are compile-time per parity of its first input row
+        const bool gp = ((c.gx0 + rA - K) & 1) != 0;
+        if (fast && gp)
+            passk_block<K, MODE, U, RED, NT, true, NA, CHAIN, 1>(A, c, wid, lane, rA, rB, voff, soff);
+        else if (fast)
+            passk_block<K, MODE, U, RED, NT, true, NA, CHAIN, 0>(A, c, wid, lane, rA, rB, voff, soff);
+        else if (gp)
+            passk_block<K, MODE, U, RED, NT, false, NA, CHAIN, 1>(A, c, wid, lane, rA, rB, voff,
+                                                                 soff);
         else
-            passk_block<K, MODE, U, RED, NT, false, NA, CHAIN>(A, c, wid, lane, rA, rB, voff,
-                                                              soff);
+            passk_block<K, MODE, U, RED, NT, false, NA, CHAIN, 0>(A, c, wid, lane, rA, rB, voff,
+                                                                 soff);
     }
 }
 
 template <int K, int MODE, int U, int NT, int NA, bool CHAIN>
 hipError_t launch_k3(bool red, const PassArgs& a, hipStream_t s) {
-    long long blocks = (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock;
+    // at least one block: a dispatch with no work (mm_prepare) still reaches the queue
+    long long blocks = std::max<long long>(1, (a.waves_total + kWavesPerBlock - 1) / kWavesPerBlock);
     if (a.xcd_remap) blocks = (blocks + 7) / 8 * 8;
     const dim3 g((unsigned)blocks), b(kBlock);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's

@@ -2,11 +2,14 @@
 // flow): K fused steps per HBM pass, the K levels spread over the P waves of a workgroup.
 //
 // The step is the generalisation of src/Model.hpp:176-235 + src/Exponencial.hpp:18-20 to
-// every cell (oracle/mm_oracle.h): per cell the neighbours' weights w = u * 8/cnt (w = u
-// where cnt = 8, 0 outside the grid), pw = w(x-1) + w(x+1), cw = pw + w(x),
-// W8 = (cw(y-1) + cw(y+1)) + pw and v' = fma(fma(u, -8, W8), r/8, u) -- the out = r*u,
-// share = out/cnt of every neighbour with r/8 factored out of the sum. Every level below is
-// that single step, so K fused levels are bit-identical to K single steps.
+// every cell (oracle/mm_oracle.h): per cell the weights w = u * 8/cnt (w = u where cnt = 8,
+// 0 outside the grid), the column triple cw of rows x-1..x+1 and the 3 x 3 box sum S of the
+// triples of columns y-1..y+1 -- each sum pairing its two rows / columns from an even
+// global index, so consecutive rows (a level's consecutive iterations) and consecutive
+// columns (a lane's column pairs) share the pair's sum -- and v' = fma(fma(u, m, S), r/8, u),
+// m = -(8 + 8/cnt) (-9 inside): the out = r*u, share = out/cnt of every neighbour with r/8
+// factored out of the sum. Every level below is that single step, so K fused levels are
+// bit-identical to K single steps.
 //
 // Why split the levels. A K-level pipeline keeps, per level and column, the shares of two
 // rows and the kept value of one (three doubles) plus the row handed to the next level.
@@ -126,9 +129,11 @@ struct WLane {
     double ownw[C]; // own as 1.0 / 0.0 (RED: the weights of the all-rows-owned groups)
 };
 
-// One level's window, per column: the weights w of the row above (wa) and of the current
-// row (wm), and the current row's values (um). FAST rows hold no wm: there w = u, so the
-// window is (wa, um) and wm is rebuilt from um when a FAST run of groups ends (wave_run).
+// One level's window, per column: wa, the weight of the row above (before an even row is
+// emitted) or the sum of the weights of the row above and the current row (the pair sum,
+// before an odd row), the current row's weights (wm) and values (um). FAST rows hold no
+// wm: there w = u, so the window is (wa, um) and wm is rebuilt from um when a FAST run of
+// groups ends (wave_run).
 template <int C>
 struct WinC {
     double wa[C], wm[C], um[C];
@@ -179,10 +184,12 @@ __device__ __forceinline__ void procc(const WLane<C>& c, long long gx, const dou
     }
 }
 
-// Level input m = 0 / 1 (row gx): fill the window.
+// Level input m = 0 / 1 (row gx): fill the window. e1: parity of the level's first emitted
+// row (the m = 1 row): odd, its window holds the pair sum of rows m = 0, 1. (e1 and wemit's
+// e are constants wherever the iteration is unrolled.)
 template <int C, int BODY>
-__device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, WinC<C>& win,
-                                      const double (&u)[C]) {
+__device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, int e1,
+                                      WinC<C>& win, const double (&u)[C]) {
     double w[C];
     procc<C, BODY>(c, gx, u, w);
 #pragma unroll
@@ -190,6 +197,7 @@ __device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, Wi
         if (m == 0) {
             win.wa[k] = w[k];
         } else {
+            if (e1) win.wa[k] = win.wa[k] + w[k];
             win.wm[k] = w[k];
             win.um[k] = u[k];
         }
@@ -197,16 +205,25 @@ __device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, Wi
 }
 
 // Level input m >= 2 (row gx): emit the window's current row (gx - 1), slide the window.
+// e: parity of the emitted row. Even: the pair sum of this row and the next, P = wm + wn,
+// gives the column triple wa + P and stays in wa for the odd row after it, whose triple is
+// P + wn (the rows paired from an even global row, oracle/mm_oracle.c triple_of). The
+// columns of a lane pair the same way (C even, the lane's first column even): box sums
+// cw(y-1) + (cw(y) + cw(y+1)) at even y, (cw(y-1) + cw(y)) + cw(y+1) at odd y.
 template <int C, int BODY>
-__device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx, WinC<C>& win,
-                                      const double (&u)[C], double (&o)[C]) {
+__device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx, int e,
+                                      WinC<C>& win, const double (&u)[C], double (&o)[C]) {
+    static_assert(C % 2 == 0, "columns paired inside a lane");
     double wn[C];
     procc<C, BODY>(c, gx, u, wn);
-    double pw[C], cw[C];
+    double cw[C], na[C];  // na: the window's next wa
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        pw[k] = win.wa[k] + wn[k];
-        cw[k] = pw[k] + (BODY == kBodyFast ? win.um[k] : win.wm[k]);
+        const double wmk = BODY == kBodyFast ? win.um[k] : win.wm[k];
+        const double pr = wmk + wn[k];  // (unused, and dropped, where e == 1)
+        const double xk = e ? wn[k] : pr;
+        cw[k] = win.wa[k] + xk;
+        na[k] = e ? wmk : pr;
     }
     double left = dpp_lower(cw[C - 1]);  // cw of column y0-1 (lane-1's last column)
     double right = dpp_upper(cw[0]);     // cw of column y0+C (lane+1's first column)
@@ -217,19 +234,40 @@ __device__ __forceinline__ void wemit(const WLane<C>& c, double r8, long long gx
         left = c.eL ? 0.0 : left;
         right = c.eR ? 0.0 : right;
     }
-    // a cell without neighbours (a 1 x 1 grid) keeps its value: m8 = 0
-    const int sxm = BODY == kBodyGen ? span3k(c.H, gx - 1) : 3;
+    // the emitted row's own-weight coefficients: -9 inside; EDGE: the grid's first / last
+    // column 8/5 (its interior rows); GEN: by the row's span (row factors) or every column's
+    // count -- 0 for a cell without neighbours (a 1 x 1 grid), which keeps its value
+    double m[C];
 #pragma unroll
-    for (int k = 0; k < C; ++k) {
+    for (int k = 0; k < C; ++k) m[k] = kM8;
+    if (BODY == kBodyEdge) {
+        m[0] = c.eL ? kM5 : m[0];
+        m[C - 1] = c.eR ? kM5 : m[C - 1];
+    } else if (BODY == kBodyGen) {
+        const int sxm = span3k(c.H, gx - 1);
+        if (!MM_WIDE_GEN_ROW || c.gen) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) m[k] = m8k(sxm * c.sy[k] - 1);
+        } else {
+            const double mr = m8k(3 * sxm - 1), me = m8k(2 * sxm - 1);
+#pragma unroll
+            for (int k = 0; k < C; ++k) m[k] = mr;
+            m[0] = c.eL ? me : mr;
+            m[C - 1] = c.eR ? me : mr;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < C; k += 2) {
         const double cl = k == 0 ? left : cw[k - 1];
-        const double cr = k == C - 1 ? right : cw[k + 1];
-        const double m8 = (BODY == kBodyGen && (!MM_WIDE_GEN_ROW || c.gen) && sxm * c.sy[k] == 1) ? 0.0 : -8.0;
-        const double t = __builtin_fma(win.um[k], m8, (cl + cr) + pw[k]);
-        o[k] = __builtin_fma(t, r8, win.um[k]);
+        const double cr = k + 1 == C - 1 ? right : cw[k + 2];
+        const double pk = cw[k] + cw[k + 1];
+        const double s0 = cl + pk, s1 = pk + cr;
+        o[k] = __builtin_fma(__builtin_fma(win.um[k], m[k], s0), r8, win.um[k]);
+        o[k + 1] = __builtin_fma(__builtin_fma(win.um[k + 1], m[k + 1], s1), r8, win.um[k + 1]);
     }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        win.wa[k] = BODY == kBodyFast ? win.um[k] : win.wm[k];
+        win.wa[k] = na[k];
         if (BODY != kBodyFast) win.wm[k] = wn[k];
         win.um[k] = u[k];
     }
@@ -276,12 +314,14 @@ template <int C, int NA>
 struct WCtx {
     WLane<C> c;
     int p, lane, rA, rB;
+    int oA;               // first output row (rA + 1 when the segment is shifted, wide_segment)
     int start;            // first iteration of this wave (p * D)
     int dmask;            // bit a: attribute a diffuses (NA > 1)
     long long g0;         // global row of input row 0 (rA - K)
     double r8[NA];        // rate / 8 of each attribute
     unsigned voff, soff, rowb;
     __amdgpu_buffer_rsrc_t in[NA], out[NA];
+    __amdgpu_buffer_rsrc_t none;  // no records: stores through it are dropped
     dv2* lds_in;          // stage p-1 (RL row slots of 32*C*NA dv2)
     dv2* lds_out;         // stage p
     const PassArgs* A;    // transfer chains (NA > 1)
@@ -426,7 +466,7 @@ __device__ __forceinline__ void pre_chain(const WCtx<C, NA>& x, double (&u)[NA][
 // One level, input m = 0 / 1: the pre-chain (NA > 1), then every attribute's window; an
 // attribute that does not diffuse in this pass emits nothing (s = 0, d = u).
 template <int C, int NA, int BODY>
-__device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
+__device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m, int e1,
                                       WinC<C> (&w)[NA], double (&u)[NA][C]) {
     pre_chain<C, NA>(x, u);
 #pragma unroll
@@ -442,7 +482,7 @@ __device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
                 }
             }
         } else {
-            wfill<C, BODY>(x.c, gx, m, w[a], u[a]);
+            wfill<C, BODY>(x.c, gx, m, e1, w[a], u[a]);
         }
     }
 }
@@ -450,7 +490,7 @@ __device__ __forceinline__ void lfill(const WCtx<C, NA>& x, long long gx, int m,
 // One level, input m >= 2: the pre-chain, every attribute's emitted row, the post-chain
 // (oracle/mm_oracle.c or_program_step's order within a pass).
 template <int C, int NA, int BODY>
-__device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C> (&w)[NA],
+__device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, int e, WinC<C> (&w)[NA],
                                       double (&u)[NA][C], double (&o)[NA][C]) {
     pre_chain<C, NA>(x, u);
 #pragma unroll
@@ -464,7 +504,7 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
                 w[a].um[k] = u[a][k];
             }
         } else {
-            wemit<C, BODY>(x.c, x.r8[a], gx, w[a], u[a], o[a]);
+            wemit<C, BODY>(x.c, x.r8[a], gx, e, w[a], u[a], o[a]);
         }
     }
     if constexpr (NA > 1 && MM_CHAIN_ASM) {
@@ -479,10 +519,15 @@ __device__ __forceinline__ void lemit(const WCtx<C, NA>& x, long long gx, WinC<C
 // MM_WIDE_ASC) -> level KW-1's row to LDS or HBM. PRO: t is a prologue iteration known at
 // compile time (level q takes part from t = kSkew*q and emits from t = kSkew*q + 2);
 // otherwise every level emits. slot: ring slot (first wave, compile time after unrolling).
+// PP: parity of the wave's p; tp: parity of t. With g0 even (wide_segment) they give every
+// level's row parities -- level q's input m = t - kSkew*q is global row g0 + p*KW + q + m,
+// its emitted row the one before -- as constants wherever the iteration is unrolled (the
+// steady groups, the prologue); elsewhere e / e1 are wave-uniform branches.
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE,
-          bool PRO, bool OWNED = false>
+          bool PRO, int PP, bool OWNED = false>
 __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st, int i,
-                                          int t, int slot) {
+                                          int t, int slot, int tp) {
+    constexpr int PK = (PP * KW) & 1;
     using G = WGeom<KW, P, B>;
     constexpr int K = G::K;
     constexpr int H2 = C / 2;       // 16-B pieces per lane, row and attribute
@@ -515,7 +560,7 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
                 for (int k = 0; k < C; ++k) cur[a][k] = x.c.sy[k] == 0 ? 0.0 : cur[a][k];
             }
         }
-        const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;
+        const unsigned o = x.voff + (unsigned)(i + U) * x.rowb;  // x.voff: row -shift
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
 #pragma unroll
@@ -554,12 +599,16 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
             for (int k = 0; k < C; ++k)
                 u[a][k] = kSkew == 2 ? cur[a][k] : (q == 0 ? uin[a][k] : st.pend[q - 1][a][k]);
         }
+        // row parities (constants once the level loop is unrolled): e1 of row g0 + j, the
+        // level's first emitted row; e of the row emitted now, gx - 1 = g0 + j + m - 2
+        const int e1 = (PK + q + 1) & 1;
+        const int e = (PK + q + 1 + tp - kSkew * q) & 1;
         if (PRO && m < 2) {
-            lfill<C, NA, BODY>(x, gx, m, st.win[q], u);
+            lfill<C, NA, BODY>(x, gx, m, e1, st.win[q], u);
             continue;
         }
         double o[NA][C];
-        lemit<C, NA, BODY>(x, gx, st.win[q], u, o);
+        lemit<C, NA, BODY>(x, gx, e, st.win[q], u, o);
         if (RED) {
             if constexpr (OWNED) {
                 // every level's row of this iteration is an output row: the lane's fixed
@@ -575,17 +624,21 @@ __device__ __forceinline__ void wave_iter(const WCtx<C, NA>& x, WState<C, NA, KW
             } else {
                 const int r = x.rA - K + m + j - 2;  // output row of level j
 #pragma unroll
-                for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.rA && r < x.rB, x.c, o[a]);
+                for (int a = 0; a < NA; ++a) accumc<C>(st.acc[q][a], r >= x.oA && r < x.rB, x.c, o[a]);
             }
         }
         if (q == KW - 1) {
-            if (kOut) {  // level K: output row m - 2 of the segment
-                const unsigned so = x.soff + (unsigned)(m - 2) * x.rowb;
+            if (kOut) {  // level K: output row m - 2 of the segment, row m - 2 - shift of out
+                const int ro = m - 2 - (x.oA - x.rA);
+                const unsigned so = x.soff + (unsigned)(ro < 0 ? 0 : ro) * x.rowb;
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
+                    // a shifted segment's first row (above its rows, wide_segment) is dropped
+                    // through a descriptor of no records (a scalar select)
+                    const __amdgpu_buffer_rsrc_t rs = ro < 0 ? x.none : x.out[a];
 #pragma unroll
                     for (int h = 0; h < H2; ++h)
-                        store_row<NT>(x.out[a], so + 16 * h, o[a][2 * h], o[a][2 * h + 1]);
+                        store_row<NT>(rs, so + 16 * h, o[a][2 * h], o[a][2 * h + 1]);
                 }
             } else {
                 dv2* dst = x.lds_out + (i % G::RL) * RW;
@@ -622,16 +675,19 @@ __device__ __forceinline__ void group_end(int i) {
 }
 
 // Steady groups [b0, b1) (multiples of B) of one wave, B iterations per loop trip (ring
-// slot i mod U: U divides B).
+// slot i mod U: U divides B). B is even, so iteration base + tt has t = i - p*D of parity
+// tt + p*D: a constant per unrolled iteration.
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int BODY, int ROLE,
-          bool OWNED = false>
+          int PP, bool OWNED = false>
 __device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st,
                                             int b0, int b1) {
+    static_assert(B % 2 == 0, "row pairs: an even number of iterations per group");
+    constexpr int PD = (PP * WGeom<KW, P, B>::D) & 1;
     for (int base = b0; base < b1; base += B) {
 #pragma unroll
         for (int tt = 0; tt < B; ++tt)
-            wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false, OWNED>(x, st, base + tt, 0,
-                                                                              tt % U);
+            wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false, PP, OWNED>(
+                x, st, base + tt, 0, tt % U, (tt + PD) & 1);
         if (P > 1) wg_sync();
     }
 }
@@ -640,7 +696,8 @@ __device__ __forceinline__ void wave_groups(const WCtx<C, NA>& x, WState<C, NA, 
 // its first group boundary, on the BODY rows' code; returns the first iteration of the
 // group loop. The first wave loads U rows ahead and starts at iteration 0 (its ring slots
 // compile-time); the others join the barriers until their start.
-template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int BODY>
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int BODY,
+          int PP>
 __device__ __forceinline__ int wave_prologue(const WCtx<C, NA>& x, WState<C, NA, KW, U>& st) {
     using G = WGeom<KW, P, B>;
     constexpr bool kIn = ROLE == kRoleFirst || ROLE == kRoleOnly;
@@ -657,9 +714,11 @@ __device__ __forceinline__ int wave_prologue(const WCtx<C, NA>& x, WState<C, NA,
 #pragma unroll
         for (int t = 0; t < G::T0; ++t) {
             if (t < G::S0)
-                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true>(x, st, t, t, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true, PP>(x, st, t, t, t % U,
+                                                                             t & 1);
             else
-                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, t, 0, t % U);
+                wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false, PP>(x, st, t, 0, t % U,
+                                                                              t & 1);
             if (P > 1 && (t + 1) % B == 0) wg_sync();
         }
         return G::T0;
@@ -667,12 +726,16 @@ __device__ __forceinline__ int wave_prologue(const WCtx<C, NA>& x, WState<C, NA,
     for (int i = 0; i < x.start; ++i) group_end<P, B>(i);
 #pragma unroll
     for (int t = 0; t < G::S0; ++t) {
-        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true>(x, st, x.start + t, t, 0);
+        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, true, PP>(x, st, x.start + t, t, 0,
+                                                                     t & 1);
         group_end<P, B>(x.start + t);
     }
+    // up to the next group boundary (fewer than B iterations; the row parities are
+    // wave-uniform values here, selects instead of constants)
     int s = x.start + G::S0;
     for (; s % B != 0; ++s) {
-        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false>(x, st, s, 0, 0);
+        wave_iter<C, NA, KW, P, U, B, RED, NT, BODY, ROLE, false, PP>(x, st, s, 0, 0,
+                                                                      (s - x.start) & 1);
         group_end<P, B>(s);
     }
     return s;
@@ -681,7 +744,8 @@ __device__ __forceinline__ int wave_prologue(const WCtx<C, NA>& x, WState<C, NA,
 // The whole schedule of one wave. MID: body of the groups whose rows are all interior.
 // RED: every level's sum of this wave's owned cells is added to carry[level][attribute]
 // (wave-uniform), so a workgroup that runs several segments sums them all.
-template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID>
+template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int ROLE, int MID,
+          int PP>
 __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
                                          double (&carry)[KW][NA]) {
     using G = WGeom<KW, P, B>;
@@ -699,8 +763,8 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
     const bool pro_mid =
         MM_WIDE_PRO_MID && !(MID == kBodyEdge && x.c.gen) && x.g0 >= 2 &&
         x.g0 + (long long)(G::T0 + (P - 1) * G::D + 2 * K + 2 * B) < x.c.H - 1;
-    const int s = pro_mid ? wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, MID>(x, st)
-                          : wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, kBodyGen>(x, st);
+    const int s = pro_mid ? wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, MID, PP>(x, st)
+                          : wave_prologue<C, NA, KW, P, U, B, RED, NT, ROLE, kBodyGen, PP>(x, st);
     if (MID == kBodyFast && pro_mid) {  // FAST rows hold no wm (w = u): GEN groups may follow
 #pragma unroll
         for (int q = 0; q < KW; ++q) {
@@ -722,21 +786,22 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
     f0 = min(f0, (long long)iend);
     f1 = max(f0, min(f1, (long long)iend));
     if (MID == kBodyEdge && x.c.gen) f0 = f1 = iend;  // a strip the EDGE body cannot run
-    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, s, (int)f0);
+    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, PP>(x, st, s, (int)f0);
     if (RED) {
         // inside the interior groups, those whose every level's output row lies in
         // [rA, rB) (level q's row: rA - K - 1 + (i - start) + p*KW - (kSkew-1) q) sum with
         // the lanes' fixed weights (wave_iter OWNED)
-        const long long r0 = x.start + K + 1 - (long long)x.p * KW + (kSkew - 1) * (KW - 1);
+        const long long r0 = x.start + K + 1 - (long long)x.p * KW + (kSkew - 1) * (KW - 1) +
+                             (x.oA - x.rA);
         const long long r1 = x.start + (x.rB - x.rA) + K + 1 - (long long)x.p * KW;
         long long m0 = (r0 + B - 1) / B * B, m1 = r1 / B * B;
         m0 = min(max(m0, f0), f1);
         m1 = max(m0, min(m1, f1));
-        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)m0);
-        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, true>(x, st, (int)m0, (int)m1);
-        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)m1, (int)f1);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, PP>(x, st, (int)f0, (int)m0);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, PP, true>(x, st, (int)m0, (int)m1);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, PP>(x, st, (int)m1, (int)f1);
     } else {
-        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE>(x, st, (int)f0, (int)f1);
+        wave_groups<C, NA, KW, P, U, B, RED, NT, MID, ROLE, PP>(x, st, (int)f0, (int)f1);
     }
     if (MID == kBodyFast && f1 > f0) {  // FAST rows hold no wm (w = u there): rebuild it
 #pragma unroll
@@ -748,7 +813,7 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
             }
         }
     }
-    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE>(x, st, (int)f1, iend);
+    wave_groups<C, NA, KW, P, U, B, RED, NT, kBodyGen, ROLE, PP>(x, st, (int)f1, iend);
     if (RED) {
         // the OWNED groups add fma(o, 0, acc) in the columns a lane does not own: lanes that
         // own none (halo lanes, lanes past the grid, which read the pitch padding) leave the
@@ -768,14 +833,19 @@ __device__ __forceinline__ void wave_run(const WCtx<C, NA>& x, int iend,
 template <int C, int NA, int KW, int P, int U, int B, bool RED, int NT, int MID>
 __device__ __forceinline__ void wave_dispatch(const WCtx<C, NA>& x, int iend,
                                               double (&carry)[KW][NA]) {
+    // the parity of p fixes the rows' parities of each role's code (wave_iter); the middle
+    // waves run one instance per parity when it matters (KW or D odd)
+    constexpr bool kMidPar = ((KW | WGeom<KW, P, B>::D) & 1) != 0;
     if (P == 1)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleOnly, MID>(x, iend, carry);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleOnly, MID, 0>(x, iend, carry);
     else if (x.p == 0)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleFirst, MID>(x, iend, carry);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleFirst, MID, 0>(x, iend, carry);
     else if (x.p == P - 1)
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleLast, MID>(x, iend, carry);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleLast, MID, (P - 1) & 1>(x, iend, carry);
+    else if (kMidPar && (x.p & 1))
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID, 1>(x, iend, carry);
     else
-        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID>(x, iend, carry);
+        wave_run<C, NA, KW, P, U, B, RED, NT, kRoleMid, MID, 0>(x, iend, carry);
 }
 
 // One strip segment [rA, rB) (local rows) of strip `strip`: this wave's part of it (level
@@ -790,7 +860,14 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
     constexpr int OC = 64 * C - 2 * C * LH;   // output columns per strip
     constexpr int RW = 32 * C * NA;           // dv2 per LDS row
     WCtx<C, NA> x;
-    x.rA = rA;
+    // Rows are paired from an even global row (wemit), and the row parities of each role's
+    // code are constants for an even g0, the segment's first input row: a segment whose g0
+    // is odd starts one row higher -- an extra first input row that loads as 0 and an extra
+    // first output row that no level-K store writes and no sum counts (its value depends
+    // on that 0 row; the rows below it do not).
+    const int sh = (int)((A.x_init + rA - K) & 1);
+    x.rA = rA - sh;
+    x.oA = rA;
     x.rB = rB;
     const long long W = A.W;
     // first loaded column: the strip's span starts C * LH columns before its first output
@@ -799,10 +876,12 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
     const long long y0 = c0 + C * lane;
     const bool in_row = y0 >= 0 && y0 < A.pitch;  // y0 % C == 0, pitch % 128 == 0
     const bool store_lane = lane >= LH && lane < 64 - LH && y0 < W;
-    x.voff = in_row ? (unsigned)(y0 * 8) : kOOBk;
+    x.rowb = (unsigned)(A.pitch * 8);
+    // input row k of the segment is row k - sh of the descriptor (base row rA - K): row -1
+    // wraps past num_records (loads 0) in every lane that loads inside the pitch
+    x.voff = (in_row ? (unsigned)(y0 * 8) : kOOBk) - (unsigned)sh * x.rowb;
     // columns past W inside the pitch are padding: writing them is harmless
     x.soff = store_lane ? (unsigned)(y0 * 8) : kOOBk;
-    x.rowb = (unsigned)(A.pitch * 8);
     x.c.H = A.H;
 #pragma unroll
     for (int k = 0; k < C; ++k) {
@@ -821,10 +900,10 @@ __device__ __forceinline__ void wide_segment(const PassArgs& A, dv2* lds, int p,
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         x.r8[a] = A.drate[a] * 0.125;
-        x.in[a] = rows_rsrc(A.in[a] + (long long)(x.rA - K) * A.pitch, x.rB - x.rA + 2 * K,
-                            A.pitch);
-        x.out[a] = rows_rsrc(A.out[a] + (long long)x.rA * A.pitch, x.rB - x.rA, A.pitch);
+        x.in[a] = rows_rsrc(A.in[a] + (long long)(rA - K) * A.pitch, rB - rA + 2 * K, A.pitch);
+        x.out[a] = rows_rsrc(A.out[a] + (long long)rA * A.pitch, rB - rA, A.pitch);
     }
+    x.none = rows_rsrc(A.out[0], 0, A.pitch);
     x.lds_in = p > 0 ? lds + (p - 1) * G::RL * RW : lds;
     x.lds_out = p < P - 1 ? lds + p * G::RL * RW : lds;
     x.A = &A;
@@ -905,12 +984,25 @@ __global__ __launch_bounds__(64 * P, MW) void mm_wide_kernel(const PassArgs A) {
 template <int C, int NA, int KW, int P, int MW, int NT>
 hipError_t wide_launch3(bool red, const PassArgs& a, hipStream_t s) {
     constexpr int U = MM_WIDE_U;
-    const dim3 g((unsigned)a.waves_total), b(64 * P);
+    // at least one workgroup: a dispatch with no work (mm_prepare) still reaches the queue
+    const dim3 g((unsigned)std::max<long long>(a.waves_total, 1)), b(64 * P);
     (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
     if (red)
         hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, true, NT>), g, b, 0, s, a);
     else
         hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, U, MM_WIDE_B, false, NT>), g, b, 0, s, a);
+    return hipGetLastError();
+}
+
+// one instance (a translation unit per instance builds in parallel: mm_wide_k20.hip)
+template <int C, int NA, int KW, int P, int MW, bool RED, int NT>
+hipError_t wide_launch4(const PassArgs& a, hipStream_t s) {
+    if (!a.seg) return hipErrorInvalidValue;
+    // at least one workgroup: a dispatch with no work (mm_prepare) still reaches the queue
+    const dim3 g((unsigned)std::max<long long>(a.waves_total, 1)), b(64 * P);
+    (void)hipGetLastError();  // the status below is this launch's, not an earlier call's
+    hipLaunchKernelGGL((mm_wide_kernel<C, NA, KW, P, MW, MM_WIDE_U, MM_WIDE_B, RED, NT>), g, b, 0,
+                       s, a);
     return hipGetLastError();
 }
 

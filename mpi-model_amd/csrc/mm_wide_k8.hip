@@ -8,6 +8,12 @@
 // the MID-body pipeline fill of round 5 the instance took 188 VGPRs, two per CU, and C2
 // fell from 1564 to 1435 GCUPS with longer segments; at 168 the steady loops are
 // unchanged (no scratch, tools/asm_steady.py), the spills sit in the GEN paths.
+// Levels in ascending order (round 6, with the box-sum step): no pend registers, and the
+// wave offset D = 2 KW + B is even, so the middle waves share one instance; the pend
+// hand-off (D = 7) takes C2 from 1722-1808 to 1531-1607 GCUPS on one box (profiles/r06/ab).
+#ifndef MM_WIDE_ASC
+#define MM_WIDE_ASC 1
+#endif
 #ifndef MM_WIDE_MIN_WAVES
 #define MM_WIDE_MIN_WAVES 3
 #endif

@@ -17,6 +17,11 @@
 #endif
 #define MM_WIDE_U 1
 #define MM_WIDE_B 2
+// levels in ascending order (round 6): no pend registers -- the sums instance spilled 455
+// VGPRs with the pend hand-off and the box-sum step, 29 without
+#ifndef MM_WIDE_ASC
+#define MM_WIDE_ASC 1
+#endif
 #define MM_CHAIN_ASM 1
 #define MM_WIDE_GEN_ROW 0  // per-column GEN weights: the row-factor body spills here (n4 p1: 125 -> 379)
 #include "mm_wide.hpp"

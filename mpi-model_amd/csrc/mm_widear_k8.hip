@@ -3,8 +3,13 @@
 // post-chain (config C5's topology): the chain's operands are compile-time registers
 // instead of an indexed register vector, and every attribute diffuses. The engine checks
 // the pattern (wring).
+// Levels in ascending order, two input rows prefetched (round 6: C5 365-368 GCUPS against
+// 327 with the pend hand-off and one row, profiles/r06/ab)
+#ifndef MM_WIDE_ASC
+#define MM_WIDE_ASC 1
+#endif
 #ifndef MM_WIDE_U
-#define MM_WIDE_U 1
+#define MM_WIDE_U 2
 #endif
 #ifndef MM_WIDE_B
 #define MM_WIDE_B 2

@@ -94,15 +94,34 @@ void or_point_apply(long long H, long long W, double* v, long long sx, long long
 }
 
 /* The whole-grid step (mm_oracle.h): every emitter's outflow is out = r*v and each of
- * its cnt neighbours receives out/cnt. Written per receiving cell c with the neighbours'
- * weights w = v * 8/cnt (w = v for cnt == 8, 0 outside the grid):
- *   v'(c) = v - r*v + sum_nbr r*v_nbr/cnt_nbr = v + (r/8) * (W8 - 8v),  W8 = sum_nbr w_nbr
- * computed as fma(fma(v, -8, W8), r/8, v) -- the multiply by r/8 factored out of the sum,
- * so an interior cell costs no multiply for its neighbours' shares. */
+ * its cnt neighbours receives out/cnt. Written per receiving cell c with the cells'
+ * weights w = v * 8/cnt (w = v for cnt == 8, 0 outside the grid) and the 3 x 3 box sum S of
+ * the weights (the cell's own weight included):
+ *   v'(c) = v - r*v + sum_nbr r*v_nbr/cnt_nbr = v + (r/8) * (S - (8 + c8) v)
+ * computed as fma(fma(v, -(8 + c8), S), r/8, v) -- the multiply by r/8 factored out of the
+ * sum, so an interior cell's neighbours cost no multiply. The box sum adds the column
+ * triples cw of three columns, each triple and the three columns paired from an even
+ * global index: cw(x,y) = w(x-1,y) + (w(x,y) + w(x+1,y)) for even x, (w(x-1,y) + w(x,y)) +
+ * w(x+1,y) for odd x, S likewise over cw(x,y-1..y+1) by the parity of y -- so two
+ * consecutive rows (columns) share the sum of their pair: the kernels add 5 fp64
+ * operations per cell where the pairwise-symmetric form took 6. */
 static inline double c8_of(int cnt) { return cnt == 8 ? 1.0 : (cnt > 0 ? 8.0 / (double)cnt : 0.0); }
 
-static inline double update_of(double v, double w8, int cnt, double r8) {
-    return cnt > 0 ? fma(fma(v, -8.0, w8), r8, v) : v;
+/* the own-weight coefficient -(8 + c8): -9 for an interior cell */
+static inline double m_of(int cnt) { return cnt > 0 ? -(8.0 + c8_of(cnt)) : 0.0; }
+
+static inline double update_of(double v, double s9, int cnt, double r8) {
+    return cnt > 0 ? fma(fma(v, m_of(cnt), s9), r8, v) : v;
+}
+
+/* the column triple of row x (parity-paired) and the box sum of column y from the
+ * padded triples cw[y .. y+2] (columns y-1 .. y+1) */
+static inline double triple_of(long long x, double a, double b, double c) {
+    return (x & 1) == 0 ? a + (b + c) : (a + b) + c;
+}
+
+static inline double box_of(long long y, const double* cw) {
+    return (y & 1) == 0 ? cw[y] + (cw[y + 1] + cw[y + 2]) : (cw[y] + cw[y + 1]) + cw[y + 2];
 }
 
 /* w row of global row gx (NULL vrow or outside grid -> +0.0) */
@@ -120,13 +139,12 @@ typedef const double* (*row_fn)(const void* ctx, long long gx);
 /* returns 0, or -1 when its row buffers cannot be allocated (nothing written) */
 static int step_rows(long long H, long long W, long long x_lo, long long x_hi,
                      row_fn rows, const void* ctx, double* vout, double rate) {
-    double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
+    double* buf = (double*)malloc(sizeof(double) * (size_t)(4 * W + 2));
     if (!buf) return -1;
     double* w_prev = buf;
     double* w_cur = buf + W;
     double* w_next = buf + 2 * W;
-    double* pw = buf + 3 * W;
-    double* cw = buf + 4 * W; /* W+2 entries, cw[y+1] for column y */
+    double* cw = buf + 3 * W; /* W+2 entries, cw[y+1] for column y */
     const double r8 = rate * 0.125;
     cw[0] = 0.0;
     cw[W + 1] = 0.0;
@@ -134,18 +152,13 @@ static int step_rows(long long H, long long W, long long x_lo, long long x_hi,
     w_row(H, W, x_lo, rows(ctx, x_lo), w_cur);
     for (long long x = x_lo; x < x_hi; ++x) {
         w_row(H, W, x + 1, rows(ctx, x + 1), w_next);
-        for (long long y = 0; y < W; ++y) {
-            pw[y] = w_prev[y] + w_next[y];
-            cw[y + 1] = pw[y] + w_cur[y];
-        }
+        for (long long y = 0; y < W; ++y) cw[y + 1] = triple_of(x, w_prev[y], w_cur[y], w_next[y]);
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
         if (v == NULL) {  /* output row outside the grid (or the slab): no cells, zeros */
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
-        } else for (long long y = 0; y < W; ++y) {
-            const double w8 = (cw[y] + cw[y + 2]) + pw[y];
-            o[y] = update_of(v[y], w8, or_neighbor_count(H, W, x, y), r8);
-        }
+        } else for (long long y = 0; y < W; ++y)
+            o[y] = update_of(v[y], box_of(y, cw), or_neighbor_count(H, W, x, y), r8);
         double* t = w_prev;
         w_prev = w_cur;
         w_cur = w_next;
@@ -199,13 +212,12 @@ static OR_FAST_TARGET void w_row_fast(long long H, long long W, long long gx,
 static OR_FAST_TARGET int step_rows_fast(long long H, long long W, long long x_lo,
                                          long long x_hi, row_fn rows, const void* ctx,
                                          double* vout, double rate) {
-    double* buf = (double*)malloc(sizeof(double) * (size_t)(5 * W + 2));
+    double* buf = (double*)malloc(sizeof(double) * (size_t)(4 * W + 2));
     if (!buf) return -1;
     double* w_prev = buf;
     double* w_cur = buf + W;
     double* w_next = buf + 2 * W;
-    double* pw = buf + 3 * W;
-    double* cw = buf + 4 * W;
+    double* cw = buf + 3 * W;
     const double r8 = rate * 0.125;
     cw[0] = 0.0;
     cw[W + 1] = 0.0;
@@ -213,9 +225,10 @@ static OR_FAST_TARGET int step_rows_fast(long long H, long long W, long long x_l
     w_row_fast(H, W, x_lo, rows(ctx, x_lo), w_cur);
     for (long long x = x_lo; x < x_hi; ++x) {
         w_row_fast(H, W, x + 1, rows(ctx, x + 1), w_next);
-        for (long long y = 0; y < W; ++y) {
-            pw[y] = w_prev[y] + w_next[y];
-            cw[y + 1] = pw[y] + w_cur[y];
+        if ((x & 1) == 0) {
+            for (long long y = 0; y < W; ++y) cw[y + 1] = w_prev[y] + (w_cur[y] + w_next[y]);
+        } else {
+            for (long long y = 0; y < W; ++y) cw[y + 1] = (w_prev[y] + w_cur[y]) + w_next[y];
         }
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
@@ -223,12 +236,15 @@ static OR_FAST_TARGET int step_rows_fast(long long H, long long W, long long x_l
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
         } else if (x > 0 && x < H - 1 && W >= 3) {
             for (long long y = 0; y < W; y += W - 1)  /* first and last column */
-                o[y] = update_of(v[y], (cw[y] + cw[y + 2]) + pw[y], or_neighbor_count(H, W, x, y), r8);
-            for (long long y = 1; y < W - 1; ++y)  /* cnt == 8 */
-                o[y] = fma(fma(v[y], -8.0, (cw[y] + cw[y + 2]) + pw[y]), r8, v[y]);
+                o[y] = update_of(v[y], box_of(y, cw), or_neighbor_count(H, W, x, y), r8);
+            for (long long y = 1; y < W - 1; y += 2) {  /* cnt == 8: odd y, then even y + 1 */
+                o[y] = fma(fma(v[y], -9.0, (cw[y] + cw[y + 1]) + cw[y + 2]), r8, v[y]);
+                if (y + 1 < W - 1)
+                    o[y + 1] = fma(fma(v[y + 1], -9.0, cw[y + 1] + (cw[y + 2] + cw[y + 3])), r8, v[y + 1]);
+            }
         } else {
             for (long long y = 0; y < W; ++y)
-                o[y] = update_of(v[y], (cw[y] + cw[y + 2]) + pw[y], or_neighbor_count(H, W, x, y), r8);
+                o[y] = update_of(v[y], box_of(y, cw), or_neighbor_count(H, W, x, y), r8);
         }
         double* t = w_prev;
         w_prev = w_cur;

@@ -15,22 +15,26 @@
  * out) to an arbitrary outflow field and is bit-for-bit the reference's single-source
  * application when the outflow is zero but at the source; with out = r*v everywhere it
  * equals or_field_step within a few ulp per step, and iterated over the bench runs' 20 and
- * 1000 steps within 2.2e-14 relative on edge-dominated grids (tests/test_oracle.py, bound
+ * 1000 steps within 3.6e-14 relative on edge-dominated grids (tests/test_oracle.py, bound
  * asserted 1e-12 = north_star's), plus invariants (conservation, flip symmetry, uniform
  * fixed point). See DESIGN.md "Oracle".
  *
  * Arithmetic contract of the whole-grid step (shared with the HIP kernels, compiled
  * -ffp-contract=off, the two fma explicit):
  *   w(c)  = v(c) * c8(c),  c8 = 8/cnt(c) rounded (1 for cnt 8: w = v), 0 outside the grid
- *   pw(c) = w(x-1,y) + w(x+1,y)
- *   cw(c) = pw(c) + w(c)
- *   W8(c) = (cw(x,y-1) + cw(x,y+1)) + pw(c)
- *   v'(c) = fma(fma(v(c), -8, W8(c)), r/8, v(c))        (cnt(c) > 0; else v' = v)
+ *   cw(c) = w(x-1,y) + (w(x,y) + w(x+1,y))   x even   (the column triple; rows paired
+ *         = (w(x-1,y) + w(x,y)) + w(x+1,y)   x odd     from an even global row)
+ *   S(c)  = cw(x,y-1) + (cw(x,y) + cw(x,y+1))   y even (the 3 x 3 box sum; columns
+ *         = (cw(x,y-1) + cw(x,y)) + cw(x,y+1)   y odd   paired from an even column)
+ *   v'(c) = fma(fma(v(c), m(c), S(c)), r/8, v(c)),  m = -(8 + c8) rounded (-9 for cnt 8)
+ *                                                     (cnt(c) > 0; else v' = v)
  * i.e. v' = v - r*v + sum_nbr r*v_nbr/cnt_nbr (Exponencial.hpp:18-20: out = r*v;
  * Model.hpp:199: share = out/cnt; Model.hpp:206-211,234: neighbours += share, source
  * -= out) with r/8 factored out of the neighbours' sum: an interior cell's neighbours
- * cost no multiply. cnt is the number of in-grid Moore neighbours (Cell.hpp:71-157 gives
- * 3/5/8 for grids of at least 2x2).
+ * cost no multiply, and a pair of rows (columns) shares the sum of its two middle
+ * weights, so a kernel adds 5 fp64 operations per cell. The step commutes with flipping
+ * an axis of even length (pairs map onto pairs). cnt is the number of in-grid Moore
+ * neighbours (Cell.hpp:71-157 gives 3/5/8 for grids of at least 2x2).
  */
 #ifndef MM_ORACLE_H
 #define MM_ORACLE_H

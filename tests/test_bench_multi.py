@@ -75,20 +75,20 @@ def test_valu_roof_mixed_plan():
     h, W = 4096, 4096
     p = [(7, 2, 2, 35), (7, 2, 2, 35), (6, 2, 2, 34)]
     v = bench.valu_roof(p, h, W, 0.08)
-    want = sum(h * k * s * (6 * c * 4 + 8) / 1024 for k, _, c, s in p) / 3
+    want = sum(h * k * s * (5 * c * 4 + 8) / 1024 for k, _, c, s in p) / 3
     assert v["cycles_per_simd_per_launch"] == round(want)
     assert v["frac"] == pytest.approx(want / (0.08e-3 * 2.4e9), rel=1e-3)
     assert bench.valu_roof([(1, 0, 1, 0)], h, W, 0.08) is None
 
 
 def test_valu_roof_four_attributes():
-    """C5's line carries a VALU roof too: per level-row of a lane 4 diffusions (6 fp64 per
-    column + 2 fp64 DPP moves each) and 4 transfers (3 fp64 per column; with run-time
-    operands no more with chain_asm) -- 320 cycles at 2 columns."""
+    """C5's line carries a VALU roof too: per level-row of a lane 4 diffusions (5 fp64 per
+    column on average + 2 fp64 DPP moves each) and 4 transfers (3 fp64 per column; with
+    run-time operands no more with chain_asm) -- 288 cycles at 2 columns."""
     import bench
-    assert bench.level_row_cycles(4) == 104
-    assert bench.level_row_cycles(2, 4, 4, 2) == 4 * (48 + 8) + 4 * 2 * 12 == 320
-    assert bench.level_row_cycles(2, 4, 4, 3) == 320
+    assert bench.level_row_cycles(4) == 88
+    assert bench.level_row_cycles(2, 4, 4, 2) == 4 * (40 + 8) + 4 * 2 * 12 == 288
+    assert bench.level_row_cycles(2, 4, 4, 3) == 288
     h, W = 4096, 4096
     info = dict(INFO, chain_kernel=2, steps_per_launch=8)
     lr = lambda k, cols: bench.level_row_cycles(cols, 4, 4, 2 if k == 8 else 1)  # noqa: E731
@@ -99,7 +99,7 @@ def test_valu_roof_four_attributes():
                         traffic=None, cons=0.0, halo="rccl", self_halo=False, lr_cycles=lr,
                         graph_captures_timed=0)
     v = d["roofline"]["valu"]
-    want = h * 8 * 37 * 320 / 1024
+    want = h * 8 * 37 * 288 / 1024
     assert v["cycles_per_simd_per_launch"] == round(want)
     assert v["frac"] == pytest.approx(want / (0.43e-3 * 2.4e9), rel=1e-3)
     assert d["config"]["graph_captures_timed"] == 0
