@@ -1540,8 +1540,23 @@ int mm_prepare(mm_engine* e, long long nsteps, long long reduce_every) {
             A.waves_total = 0;
             A.waves_a = -1;  // the priming mark (mm::launch_passk / launch_wide)
             MM_TRY(launch_timed(e, red, A, 0, false, wide ? -(int)k : (int)k));
+            // a split pass also launches its border rows on the comm stream, another queue
+            // with its own scratch: unprimed, the first border launch of a 20-step run
+            // blocked the host for 1.5 ms (8192 x 32768 self-halo, profiles/r06/trace20)
+            if (e->split && e->d.h >= 2 * k + 1) {
+                mm::PassArgs B = A;
+                if (wide) {
+                    MM_HIP(mm::launch_wide((int)k, wcols(e, (int)k), e->na, red, B, e->s_comm,
+                                           wvar(e)));
+                } else {
+                    B.seg = 0;
+                    B.th = mm::kBorderRows;
+                    MM_HIP(mm::launch_passk((int)k, e->na, red, B, e->s_comm, 0));
+                }
+            }
         }
         MM_HIP(hipStreamSynchronize(e->s_comp));
+        if (e->split) MM_HIP(hipStreamSynchronize(e->s_comm));
     }
     return MM_OK;
 }
