@@ -535,16 +535,16 @@ constexpr int kWideSmallAuto = 8;
 double slab_cells(const mm_engine* e) { return (double)e->min_rows * (double)e->d.W; }
 
 // the K = 20 planner's slabs (forced MM_WIDE=1 plans every slab that way)
-// Slabs of 2^27 - 2^28 cells in a halo chain (the 4096 x 32768 slabs of an 8-GPU c3 run)
-// also take the K = 20 planner: with the interior / border split the level-split kernel's
-// one K = 20 pass runs 20 steps in 1.33 ms against 1.40 for mm_passk_kernel's 7 + 7 + 6
-// (2030 vs 1913 GCUPS, `bench.py --self-halo`, 3 rounds each, profiles/r04/midslab);
-// without a halo mm_passk_kernel stays ahead there (2050 vs ~1920).
+// Slabs of 2^27 - 2^28 cells (the 4096 x 32768 slabs of an 8-GPU c3 run) also take the
+// K = 20 planner. Round 4 kept mm_passk_kernel there without a halo (2050 vs ~1920 GCUPS,
+// profiles/r04/midslab); since the box-sum step the level-split kernel runs the split
+// 4096 x 32768 slab at 2532 GCUPS against 1194-1272 for mm_passk_kernel's 7 + 7 + 6 without
+// one (20 steps, profiles/r06/self20, profiles/r06/selfhalo).
 constexpr double kWideSplitCells = 134217728.0;  // 2^27
 
 bool wide_big(const mm_engine* e) {
     return e->wide > 0 || slab_cells(e) >= kWideCells ||
-           (e->wide < 0 && e->split && e->na == 1 && slab_cells(e) >= kWideSplitCells);
+           (e->wide < 0 && e->na == 1 && slab_cells(e) >= kWideSplitCells);
 }
 
 bool wide_on(const mm_engine* e) {

@@ -207,7 +207,7 @@ __device__ __forceinline__ void wfill(const WLane<C>& c, long long gx, int m, in
 // Level input m >= 2 (row gx): emit the window's current row (gx - 1), slide the window.
 // e: parity of the emitted row. Even: the pair sum of this row and the next, P = wm + wn,
 // gives the column triple wa + P and stays in wa for the odd row after it, whose triple is
-// P + wn (the rows paired from an even global row, oracle/mm_oracle.c triple_of). The
+// P + wn (the rows paired from an even global row, oracle/mm_oracle.h). The
 // columns of a lane pair the same way (C even, the lane's first column even): box sums
 // cw(y-1) + (cw(y) + cw(y+1)) at even y, (cw(y-1) + cw(y)) + cw(y+1) at odd y.
 template <int C, int BODY>

@@ -114,11 +114,8 @@ static inline double update_of(double v, double s9, int cnt, double r8) {
     return cnt > 0 ? fma(fma(v, m_of(cnt), s9), r8, v) : v;
 }
 
-/* the column triple of row x (parity-paired) and the box sum of column y from the
- * padded triples cw[y .. y+2] (columns y-1 .. y+1) */
-static inline double triple_of(long long x, double a, double b, double c) {
-    return (x & 1) == 0 ? a + (b + c) : (a + b) + c;
-}
+/* the box sum of column y from the padded column triples cw[y .. y+2] (columns y-1 .. y+1),
+ * paired from an even column */
 
 static inline double box_of(long long y, const double* cw) {
     return (y & 1) == 0 ? cw[y] + (cw[y + 1] + cw[y + 2]) : (cw[y] + cw[y + 1]) + cw[y + 2];
@@ -152,13 +149,24 @@ static int step_rows(long long H, long long W, long long x_lo, long long x_hi,
     w_row(H, W, x_lo, rows(ctx, x_lo), w_cur);
     for (long long x = x_lo; x < x_hi; ++x) {
         w_row(H, W, x + 1, rows(ctx, x + 1), w_next);
-        for (long long y = 0; y < W; ++y) cw[y + 1] = triple_of(x, w_prev[y], w_cur[y], w_next[y]);
+        if ((x & 1) == 0) {  /* the column triples, rows paired from an even row */
+            for (long long y = 0; y < W; ++y) cw[y + 1] = w_prev[y] + (w_cur[y] + w_next[y]);
+        } else {
+            for (long long y = 0; y < W; ++y) cw[y + 1] = (w_prev[y] + w_cur[y]) + w_next[y];
+        }
         const double* v = rows(ctx, x);
         double* o = vout + (x - x_lo) * W;
         if (v == NULL) {  /* output row outside the grid (or the slab): no cells, zeros */
             for (long long y = 0; y < W; ++y) o[y] = 0.0;
-        } else for (long long y = 0; y < W; ++y)
-            o[y] = update_of(v[y], box_of(y, cw), or_neighbor_count(H, W, x, y), r8);
+        } else {
+            long long y = 0;
+            for (; y + 1 < W; y += 2) {  /* box_of of an even column and the odd one after it */
+                const double p = cw[y + 1] + cw[y + 2];
+                o[y] = update_of(v[y], cw[y] + p, or_neighbor_count(H, W, x, y), r8);
+                o[y + 1] = update_of(v[y + 1], p + cw[y + 3], or_neighbor_count(H, W, x, y + 1), r8);
+            }
+            if (y < W) o[y] = update_of(v[y], box_of(y, cw), or_neighbor_count(H, W, x, y), r8);
+        }
         double* t = w_prev;
         w_prev = w_cur;
         w_cur = w_next;

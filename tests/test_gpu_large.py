@@ -182,25 +182,26 @@ def test_c4_production_pass_full_grid(gpu, O, monkeypatch):
     driver_run_bands(gpu, O, monkeypatch, 16384, 16384, 1, [20])
 
 
-def test_mid_slab_in_a_chain_takes_the_k20_planner(gpu):
-    """Slabs of 2^27 - 2^28 cells with a halo (rank 0 of an 8-rank c3 chain: 4096 x 32768)
-    plan the level-split kernel's K = 20 pass -- with the interior / border split it beats
-    mm_passk_kernel's 7 + 7 + 6 (profiles/r04/midslab); the same slab alone keeps them."""
+def test_mid_slab_takes_the_k20_planner(gpu):
+    """Slabs of 2^27 - 2^28 cells (rank 0 of an 8-rank c3 chain: 4096 x 32768) plan the
+    level-split kernel's K = 20 pass, with a halo (the interior / border split) and, since
+    the box-sum kernels, without one (profiles/r06/self20: 2532 GCUPS split against 1194
+    for mm_passk_kernel's 7 + 7 + 6)."""
     with gpu.Engine(32768, 32768, 0, 4096, rank=0, nranks=8, halo_mode=gpu.MM_HALO_HOST) as e:
         e.add_diffuse(0, RATE)
         assert e.pass_plan(20) == [20]
         assert e.pass_kernel(20)[0] == 3 and e.info()["halo_depth"] == 20
     with gpu.Engine(4096, 32768) as e:
         e.add_diffuse(0, RATE)
-        assert e.pass_plan(20) == [7, 7, 6] and e.info()["kernel"] == 2
+        assert e.pass_plan(20) == [20] and e.info()["kernel"] == 3
 
 
-def test_standalone_mid_slab_keeps_passk(gpu, O, monkeypatch):
-    """A standalone 4096 x 32768 grid (2^27 cells, NO halo -- not the slab of an N = 8 c3
-    rank: that one takes the level-split kernel's K = 20 pass with the interior / border
-    split, tests/test_gpu_fullsize.py c3_n8): the default planner's 20 steps are
-    mm_passk_kernel passes of 7 + 7 + 6."""
-    driver_run_bands(gpu, O, monkeypatch, 4096, 32768, 0, [7, 7, 6])
+def test_standalone_mid_slab_takes_k20(gpu, O, monkeypatch):
+    """A standalone 4096 x 32768 grid (2^27 cells, NO halo -- the slab of an N = 8 c3 rank
+    without its interior / border split, tests/test_gpu_fullsize.py c3_n8): the default
+    planner's 20 steps are one K = 20 pass of the level-split kernel (round 4 kept
+    mm_passk_kernel's 7 + 7 + 6 here; the box-sum kernels run it twice as fast)."""
+    driver_run_bands(gpu, O, monkeypatch, 4096, 32768, 1, [20])
 
 
 # ---- C5 at the size it is benchmarked at (bench.py --workload c5) ------------------------
