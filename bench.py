@@ -437,7 +437,8 @@ def main():
         kname = {0: "mm_pass_kernel", 2: "mm_passk_kernel", 3: "mm_wide_kernel"}[info["kernel"]]
         traffic, traffic_src = None, None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):  # only when it was measured on this kernel
+        # only when it was measured on this kernel and on the workload's own grid
+        if os.path.exists(tf) and not args.grid:
             with open(tf) as f:
                 pmc = json.load(f)
             key = f"{args.workload}_n{N}_k{spl}"

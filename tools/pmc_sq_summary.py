@@ -6,7 +6,8 @@ MI355X_MICROARCH.md 'rocprofv3 PMC slots'), plus the effective clock GRBM_GUI_AC
 / kernel duration when a kernel-trace average is given -- only for dispatches of at least
 0.3 ms: GRBM_GUI_ACTIVE counts busy cycles across the dispatch boundaries, so on shorter
 dispatches the quotient reads high (MI355X_MICROARCH.md 'DVFS give-back'; round 5's C2
-figure of 2.59 GHz on 71 us dispatches was above the part's 2.4 GHz maximum)."""
+figure of 2.59 GHz on 71 us dispatches was above the part's 2.4 GHz maximum). Dispatches of
+a single workgroup (mm_prepare's priming of a kernel, no work) are left out."""
 import csv
 import glob
 import json
@@ -23,6 +24,8 @@ def main():
         with open(f) as fh:
             rows.extend(csv.DictReader(fh))
     rows = [r for r in rows if "mm_pass" in r.get("Kernel_Name", "") or "mm_wide" in r.get("Kernel_Name", "")]
+    # mm_prepare's priming dispatches (one workgroup of no work) are not passes
+    rows = [r for r in rows if r.get("Grid_Size") is None or r.get("Grid_Size") != r.get("Workgroup_Size")]
     if not rows:
         sys.exit("no step-kernel dispatches")
     by_kernel = {}

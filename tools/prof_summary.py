@@ -40,10 +40,17 @@ def bench_line(path):
         return None
 
 
+def priming(r):
+    """mm_prepare's priming dispatch of a kernel: one workgroup, no work (not a pass)."""
+    g = r.get("Grid_Size_X", r.get("Grid_Size"))
+    w = r.get("Workgroup_Size_X", r.get("Workgroup_Size"))
+    return g is not None and g == w
+
+
 def steady(trace, name):
     """Durations (us) of `name`'s dispatches in start order, and the steady-state window."""
     d = sorted(((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-                for r in trace if r.get("Kernel_Name") == name))
+                for r in trace if r.get("Kernel_Name") == name and not priming(r)))
     durs = [x for _, x in d]
     skip = max(3, len(durs) // 10) if len(durs) > 6 else 0
     return durs, durs[skip:], skip
@@ -70,6 +77,12 @@ def main():
     line = bench_line(os.path.join(d, "trace.log"))
     if name and trace:
         durs, st, skip = steady(trace, name)
+        # the kernel's own statistics without priming dispatches (kernel_stats.csv counts them)
+        if durs:
+            res["calls"] = len(durs)
+            res["avg_us"] = statistics.mean(durs)
+            res["min_us"] = min(durs)
+            res["max_us"] = max(durs)
         if st:
             res["steady_dispatches"] = len(st)
             res["steady_skipped_first"] = skip
@@ -99,7 +112,8 @@ def main():
             res["steady_frac_vs_bench"] = res["steady_frac"] / line["roofline"]["frac"]
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
-                if name and r.get("Kernel_Name", "") == name and r.get("Counter_Name") == counter]
+                if name and r.get("Kernel_Name", "") == name and r.get("Counter_Name") == counter
+                and not priming(r)]
         if vals:
             res[counter + "_KB_avg"] = statistics.mean(vals)
             res[counter + "_dispatches"] = len(vals)
