@@ -390,17 +390,23 @@ void set_ranges(mm::PassArgs& A, long long lo, long long hi, long long lo2, long
 // k-1 read; ghost rows are only touched on comm; the rows an exchange sends were written
 // by the border kernel before it. With the host transport the caller has already put the
 // neighbours' rows into the ghost rows, and the same schedule runs without the exchange.
-int split_begin(mm_engine* e, int depth) {
-    if (e->comm_live) {
-        MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
-    } else {
-        // first split pass of the run: the border work follows all earlier compute work
-        MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
-        MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
-    }
+// A split pass in two halves, the compute stream's first: the interior rows need only the
+// previous border rows, not this pass's exchange, so their launch goes ahead of the
+// exchange's host-side enqueue (an RCCL group call took 64 us before the interior's launch
+// in profiles/r06/trace20).
+int split_comp(mm_engine* e) {
+    // interior k reads the rows border k-1 wrote
+    if (e->comm_live) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
+    // everything the compute stream ran before interior k: interior k-1, the fills
+    MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
+    return MM_OK;
+}
+
+int split_comm(mm_engine* e, int depth) {
+    // first split pass of the run: the exchange follows all earlier compute work
+    if (!e->comm_live) MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
     if (rccl_halo(e)) MM_TRY(halo_rccl(e, depth));  // needs only border k-1 (same stream)
     // border k reads rows interior k-1 wrote (and reuses the partials finalize k-1 read)
-    MM_HIP(hipEventRecord(e->ev_comp_mark, e->s_comp));
     MM_HIP(hipStreamWaitEvent(e->s_comm, e->ev_comp_mark, 0));
     return MM_OK;
 }
@@ -426,18 +432,19 @@ int enqueue_pass(mm_engine* e, const Pass& p, bool red, bool time_it) {
     fill_args(e, p, A);
     long long total_waves = 0;
     if (e->split && h >= 2 * depth + 1) {
-        MM_TRY(split_begin(e, depth));
+        MM_TRY(split_comp(e));
         set_ranges(A, depth, h - depth, 0, 0);
         const long long interior_waves = A.waves_total;
         mm::PassArgs B = A;
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, 0));
+        MM_TRY(split_comm(e, depth));
         B.th = 1;  // border: short row blocks, the launch is latency-bound
         set_ranges(B, 0, depth, h - depth, h);
         B.partial_base = interior_waves;
         MM_HIP(mm::launch_pass(e->na, red, B, e->s_comm, e->variant));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
-        A.partial_base = 0;
-        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, 0));
         total_waves = interior_waves + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
@@ -634,10 +641,13 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     A.nstrips = (int)nstrips_wide(e, k);
     long long total_blocks = 0;  // partials units: one per workgroup
     if (e->split && h >= 2 * depth + 1) {
-        MM_TRY(split_begin(e, depth));
+        MM_TRY(split_comp(e));
         wide_range(e, k, red, A, depth, h - depth);
         const long long interior = A.waves_total;
         mm::PassArgs B = A;
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
+        MM_TRY(split_comm(e, depth));
         B.th = B.th_edge = depth;
         B.ra0 = 0;
         B.ra1 = depth;
@@ -649,8 +659,6 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
         MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, wvar(e)));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
-        A.partial_base = 0;
-        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
         total_blocks = interior + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
@@ -682,10 +690,13 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
     A.xcd_remap = e->xcd;
     long long total_waves = 0;
     if (e->split && h >= 2 * depth + 1) {
-        MM_TRY(split_begin(e, depth));
+        MM_TRY(split_comp(e));
         seg_range(e, k, red, A, depth, h - depth);
         const long long interior_waves = A.waves_total;
         mm::PassArgs B = A;
+        A.partial_base = 0;
+        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, k));
+        MM_TRY(split_comm(e, depth));
         B.seg = 0;
         B.th = mm::kBorderRows;  // border: short row blocks, the launch is latency-bound
         B.xcd_remap = 0;
@@ -694,8 +705,6 @@ int enqueue_passk(mm_engine* e, int k, int mask, bool time_it) {
         MM_HIP(mm::launch_passk(k, e->na, red, B, e->s_comm, 0));
         MM_HIP(hipEventRecord(e->ev_comm_done, e->s_comm));
         e->comm_live = true;
-        A.partial_base = 0;
-        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, k));
         total_waves = interior_waves + B.waves_total;
         if (red) MM_HIP(hipStreamWaitEvent(e->s_comp, e->ev_comm_done, 0));
     } else {
