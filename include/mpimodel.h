@@ -246,8 +246,10 @@ int mm_point_apply_strict(mm_engine* eng, int attr, long long sx, long long sy,
  * same interior / border split as with RCCL. */
 int mm_run(mm_engine* eng, long long nsteps, long long reduce_every);
 /* Do the one-time work of a following mm_run(eng, nsteps, reduce_every) now -- capture and
- * instantiate its hipGraph, plan its eager tail passes (loading their kernels) -- without
- * running any step. Optional: mm_run does the same work on first use. */
+ * instantiate its hipGraph, plan its eager tail passes and dispatch each of their kernels
+ * once with no work on every stream the run uses (which loads the kernel and sizes that
+ * queue's scratch) -- without running any step: no buffer is read or written. Optional:
+ * mm_run does the same work on first use, except the empty dispatches. */
 int mm_prepare(mm_engine* eng, long long nsteps, long long reduce_every);
 /* The kernel passes mm_run(eng, nsteps, .) launches: *count passes, the steps of the first
  * min(*count, cap) in lens[] (K-step passes; 1 per step for the one-step kernel). Host-only
