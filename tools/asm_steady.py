@@ -2,7 +2,8 @@
 """Steady-state loops of one wide-kernel instance in a hipcc -S file: for each loop whose
 body holds the full level work of B rows (dpp count = 4 x levels x rows), its instruction
 mix (tools/asm_loops.py's counters) -- the evidence that the production loops issue the
-modelled 24 fp64 + 4 DPP per level-row (6 per cell, round 5) and no scratch.
+modelled 20 fp64 + 4 DPP per level-row on average (5 per cell: the box-sum step of round 6,
+22 on an even row and 18 on the odd row after it) and no scratch.
 
 usage: asm_steady.py FILE.s KERNEL_SUBSTRING DPP_PER_TRIP
 """
@@ -30,7 +31,7 @@ def main():
         if tgt in labels and labels[tgt] < i:
             c = mix(body[labels[tgt]:i + 1])
             key = tuple(sorted(c.items()))
-            if c.get("dpp") == dpp and c.get("f64", 0) == 6 * dpp and key not in seen:
+            if c.get("dpp") == dpp and c.get("f64", 0) == 5 * dpp and key not in seen:
                 seen.add(key)
                 role = "first wave (loads)" if c.get("bload") else (
                     "last wave (stores)" if c.get("bstore") else "middle wave (LDS in/out)")

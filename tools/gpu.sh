@@ -18,8 +18,11 @@
 #   bash tools/gpu.sh selfhalo                bench.py --self-halo beside the plain run on the
 #                                             slab shapes of the N > 1 runs (price of the
 #                                             interior / border split + RCCL exchange)
-#   bash tools/gpu.sh final                   a round's evidence on the committed tree: test, lines,
-#                                             then prof of each line's own plan and length
+#   bash tools/gpu.sh final                   a round's evidence on the committed tree: test, lines
+#                                             (FINAL_PART=a), then prof / sq / L2 counters of each
+#                                             line's own plan and length (FINAL_PART=b)
+#   bash tools/gpu.sh self20                  every scaling slab plain and --self-halo at 20 steps
+#   bash tools/gpu.sh trace20                 HIP-runtime trace of a 20-step split run
 #   bash tools/gpu.sh ab TAG WL STEPS REPS "ENV_A" "ENV_B" [bench.py args]
 #                                             A/B of two environments on one box, alternating
 #                                             A B A B ... REPS times (GCUPS per run)
@@ -132,15 +135,40 @@ selfhalo() {
     done
 }
 
-final() {
-    gpu_test
-    lines
-    prof c3_k20 c3 20 5
-    prof c4_k20 c4 1000 50
-    prof c2_k8 c2 1000 50
-    prof c5_k8 c5 1000 50
-    sq c3_k20 c3 20 5
-    sq c2 c2 1000 50
+final() {  # part a (FINAL_PART=a, default): suite + lines; part b: profiles (each fits a call)
+    if [ "${FINAL_PART:-a}" = a ]; then
+        gpu_test
+        lines
+        MM_CHAIN_RING=0 TAG=runtime_chain bench c5 1000 50
+        TAG=4096x32768 bench c3 20 5 --grid 4096 32768 --no-cpu-baseline
+    else
+        prof c3_k20 c3 20 5
+        prof c4_k20 c4 1000 50
+        prof c2_k8 c2 1000 50
+        prof c5_k8 c5 1000 50
+        sq c3_k20 c3 20 5
+        sq c2 c2 1000 50
+        sq c5_k8 c5 1000 50
+        pmc c3tcc c3 20 5 "TCC_HIT_sum TCC_MISS_sum"
+    fi
+}
+
+self20() {  # the split's price at the driver's 20 steps: every scaling slab plain and split
+    local g
+    for g in "32768 32768" "16384 32768" "8192 32768" "4096 32768" "16384 16384"; do
+        set -- $g
+        TAG="${1}x${2}_plain" bench c3 20 5 --grid $1 $2 --no-cpu-baseline
+        TAG="${1}x${2}_self" bench c3 20 5 --grid $1 $2 --no-cpu-baseline --self-halo
+    done
+}
+
+trace20() {  # HIP-runtime + kernel trace of one 20-step split run (launch-to-start latencies)
+    local out="$D/hiptrace20"
+    mkdir -p "$out"
+    timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$out" -o run \
+        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --grid 8192 32768 --self-halo \
+        > "$out/trace.log" 2>&1 || fail trace20 $? "$out/trace.log"
+    python3 tools/launch_latency.py "$out" > "$out/launch_latency.txt" && cat "$out/launch_latency.txt"
 }
 
 ab() {  # TAG WL STEPS REPS ENVA ENVB [args]
@@ -211,6 +239,8 @@ case "$cmd" in
     trace) trace "$@" ;;
     pmc) pmc "$@" ;;
     selfhalo) selfhalo ;;
+    self20) self20 ;;
+    trace20) trace20 ;;
     thin) thin ;;
     thintrace) thintrace ;;
     ab) ab "$@" ;;
