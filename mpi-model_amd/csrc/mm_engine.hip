@@ -108,6 +108,7 @@ struct mm_engine {
     bool plan = true;        // pass-length planner (MM_PASS_PLAN=0: balanced passes of K)
     double seg_waves = 0.0;  // segment waves per resident wave slot (MM_SEG_WAVES; 0: auto)
     double seg_edge = 0.0;   // edge-strip segment length / interior length (MM_SEG_EDGE; 0: auto)
+    bool border_segments = true;  // wide split passes: full-length border segments (MM_BORDER_SEGMENTS)
     int xcd = 0;             // XCD-contiguous block order (MM_XCD_REMAP, mm_passk_kernel)
     int ncu = 0;             // compute units of the device
     int wpc[2][2][mm::kMaxAttr + 1][mm::kMaxSteps + 1] = {};  // segment kernel waves/CU cache
@@ -642,18 +643,29 @@ int enqueue_wide(mm_engine* e, int k, int mask, bool time_it) {
     long long total_blocks = 0;  // partials units: one per workgroup
     if (e->split && h >= 2 * depth + 1) {
         MM_TRY(split_comp(e));
-        wide_range(e, k, red, A, depth, h - depth);
+        // The rows that read the exchanged ghost rows, [0, K) and [h-K, h), run on the comm
+        // stream after the exchange. By default as the top and bottom segments of every
+        // strip at the slab plan's full segment length T (what the unsplit plan would run
+        // there), the rest of the plan now: a K-row border segment paid the K = 20 pipeline
+        // fill (~94 iterations) for 20 rows beside the interior (MM_BORDER_SEGMENTS=0).
+        long long T = depth;
+        if (e->border_segments) {
+            mm::PassArgs P = A;
+            wide_range(e, k, red, P, 0, h);
+            T = std::min<long long>(std::max<long long>(P.th, depth), h / 2);
+        }
+        wide_range(e, k, red, A, T, h - T);
         const long long interior = A.waves_total;
         mm::PassArgs B = A;
         A.partial_base = 0;
-        MM_TRY(launch_timed(e, red, A, h - 2 * depth, time_it, -k));
+        MM_TRY(launch_timed(e, red, A, h - 2 * T, time_it, -k));
         MM_TRY(split_comm(e, depth));
-        B.th = B.th_edge = depth;
+        B.th = B.th_edge = (int)T;
         B.ra0 = 0;
-        B.ra1 = depth;
-        B.rb0 = (int)(h - depth);
+        B.ra1 = (int)T;
+        B.rb0 = (int)(h - T);
         B.rb1 = (int)h;
-        B.waves_a = seg_wave_count(depth, B.nstrips, depth, depth);
+        B.waves_a = seg_wave_count(T, B.nstrips, T, T);
         B.waves_total = 2 * B.waves_a;
         B.partial_base = interior;
         MM_HIP(mm::launch_wide(k, wcols(e, k), e->na, red, B, e->s_comm, wvar(e)));
@@ -1176,6 +1188,7 @@ int mm_engine_create(const mm_desc* desc, mm_engine** out) {
         if (v > 0.0 && v <= 1.0) e->seg_edge = v;
     }
     if (const char* x = std::getenv("MM_XCD_REMAP")) e->xcd = std::atoi(x) != 0;
+    if (const char* b = std::getenv("MM_BORDER_SEGMENTS")) e->border_segments = std::atoi(b) != 0;
     if (const char* r = std::getenv("MM_CHAIN_RING")) e->ring_ok = std::atoi(r) != 0;
     if (const char* r = std::getenv("MM_SYNC_SPIN")) e->sync_spin = std::atoi(r) != 0;
     // non-temporal stores pay once the two buffers outgrow the 256 MiB Infinity Cache
