@@ -194,7 +194,9 @@ int mm_device_synchronize(int device);
  * kernel; fixes K), MM_PASS_PLAN=0
  * (balanced passes of K, no planner), MM_ROWS_PER_WAVE (8/16/32),
  * MM_SEG_WAVES, MM_SEG_EDGE, MM_XCD_REMAP (mm_passk_kernel's block order only; the
- * level-split kernel keeps the hardware order) and MM_KERNEL_VARIANT (non-temporal stores;
+ * level-split kernel keeps the hardware order), MM_BORDER_SEGMENTS=0 (the level-split
+ * kernel's split passes with K-row border segments instead of full-length top / bottom
+ * segments) and MM_KERNEL_VARIANT (non-temporal stores;
  * the four-attribute K = 8 instances always store non-temporal) override tuning;
  * MM_SELF_HALO=1 with MM_HALO_RCCL and nranks == 1 makes the rank
  * exchange border rows with itself (ghost rows outside the grid: exercises the RCCL
