@@ -564,6 +564,49 @@ def test_rccl_halo_path_many_steps(gpu, O, monkeypatch):
     assert np.array_equal(got, O.field_step(O.fill_random(H, W), RATE, steps=steps))
 
 
+@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("G", [1, 2])
+def test_prepare_primes_eager_passes_without_running(gpu, O, monkeypatch, wide, G):
+    """mm_prepare's priming: with graphs off, every planned pass is eager, and prepare
+    dispatches each planned kernel once with no work -- on the compute stream, and on the
+    comm stream for a split slab (G = 2: host-halo chain) -- without touching a buffer."""
+    H, W, steps = 240, 700, 17
+    monkeypatch.setenv("MM_GRAPH", "0")
+    monkeypatch.setenv("MM_WIDE", str(wide))
+    monkeypatch.setenv("MM_STEPS_PER_PASS", "8" if wide else "6")
+    es = []
+    try:
+        for g in range(G):
+            x0, h = gpu.partition_rows(H, G, g)
+            es.append(gpu.Engine(H, W, x0, h, rank=g, nranks=G,
+                                 halo_mode=gpu.MM_HALO_HOST if G > 1 else 0))
+        for e in es:
+            e.fill_random(0)
+            e.add_diffuse(0, 0.2)
+        plan = es[0].pass_plan(steps)
+        for e in es:
+            if G == 1:
+                e.prepare(steps)
+            else:  # the host transport runs one pass per call: prepare each pass length
+                for k in sorted(set(plan)):
+                    e.prepare(k)
+            assert e.info()["steps_done"] == 0
+        assert np.array_equal(np.vstack([e.download() for e in es]), O.fill_random(H, W))
+        for k in plan:
+            if G > 1:
+                halos = [e.halo_export(k) for e in es]
+                for g, e in enumerate(es):
+                    e.halo_import(halos[g - 1][1] if g > 0 else None,
+                                  halos[g + 1][0] if g < G - 1 else None, nrows=k)
+            for e in es:
+                e.run(k)
+        got = np.vstack([e.download() for e in es])
+    finally:
+        for e in es:
+            e.close()
+    assert np.array_equal(got, O.field_step(O.fill_random(H, W), 0.2, steps=steps))
+
+
 @pytest.mark.parametrize("warmup", [0, 3])
 def test_prepare_captures_graph_without_running(gpu, O, warmup):
     # mm_prepare does a run's one-time work (graph capture for both buffer parities, tail
